@@ -1,0 +1,42 @@
+"""Shared parity helpers (the comparison rule of SURVEY.md §8c)."""
+import glob
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
+               if os.path.basename(f)[:-4] not in ("shapes", "generators"))
+
+
+def load_case(name):
+    d = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    spec = json.loads(str(d["system_json"]))
+    return spec, d["rays_in"], d["history"]
+
+
+def compare(got, ref, rtol):
+    """NaN masks must be equal element for element; finite values must satisfy
+    |got - ref| <= rtol * max(|ref|, colmax) where colmax is the max |finite ref| of that column in
+    that plane (column-scaled tolerance).  Returns (ok, report dict)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if got.shape != ref.shape:
+        return False, {"shape": (got.shape, ref.shape)}
+    nan_g, nan_r = np.isnan(got), np.isnan(ref)
+    mask_flips = int((nan_g != nan_r).sum())
+    fin = ~nan_g & ~nan_r
+    absref = np.where(np.isfinite(ref), np.abs(ref), 0.0)
+    colmax = absref.max(axis=-2, keepdims=True) if ref.ndim >= 2 else absref.max()
+    scale = np.maximum(absref, colmax)
+    err = np.where(fin, np.abs(got - ref), 0.0)
+    inf_mismatch = int((fin & (np.isinf(got) | np.isinf(ref)) & (got != ref)).sum())
+    err = np.where(np.isinf(err), 0.0, err)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.where(scale > 0, err / scale, err)
+    max_rel = float(rel.max()) if rel.size else 0.0
+    n_bit_diff = int((fin & (got != ref)).sum())
+    ok = mask_flips == 0 and inf_mismatch == 0 and max_rel <= rtol
+    return ok, {"mask_flips": mask_flips, "max_rel": max_rel, "n_values_not_bitwise": n_bit_diff,
+                "inf_mismatch": inf_mismatch}

@@ -1,0 +1,44 @@
+"""The NumPy oracle reproduces the reference's own outputs (golden vectors) BIT FOR BIT."""
+import numpy as np
+import pytest
+
+from oracle import rt_numpy as O
+from parity import CASES, load_case
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference_bitwise(name):
+    spec, rays, ref = load_case(name)
+    got = O.ray_trace(spec["surfaces"], spec["materials"], rays)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref, equal_nan=True)
+
+
+def test_oracle_input_ranks():
+    import json, os
+    from parity import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "shapes.npz"))
+    spec = json.loads(str(d["system_json"]))
+    for k in ("1", "2", "3"):
+        got = O.ray_trace(spec["surfaces"], spec["materials"], d["rays" + k])
+        assert np.array_equal(got, d["out" + k], equal_nan=True), k
+
+
+def test_oracle_generators():
+    import os
+    from parity import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "generators.npz"))
+    assert np.array_equal(O.ray_fan([1., 2., 3.], 0.3, 7, 0.5, nphis=5), d["fan"])
+
+
+def test_golden_cases_exercise_edge_semantics():
+    """The fixtures must contain the per-ray failure modes the kernel has to reproduce."""
+    _, _, h = load_case("tir_prism")
+    # TIR: refracted plane keeps phase and wavelength but position is NaN (RT:1221)
+    tir = np.isnan(h[4, :, 0]) & ~np.isnan(h[4, :, 6]) & ~np.isnan(h[4, :, 7])
+    assert tir.sum() > 0
+    _, _, h = load_case("stress")
+    miss = np.isnan(h[:, :, 0]) & ~np.isnan(h[:, :, 3])      # sphere miss keeps d and wavelength
+    assert miss.sum() > 0
+    _, _, h = load_case("c4_opm")
+    assert np.isnan(h[-1]).all(axis=1).sum() > 0              # NA clip of PerfectLens (RT:1757-1760)
