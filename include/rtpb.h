@@ -1,0 +1,153 @@
+/*
+ * rtpb.h -- C ABI of the MI355X-native sequential ray tracer (ray_trace_pb_amd).
+ *
+ * This is the drop-in boundary for the reference's hot path, QI2lab/ray_trace_pb @ 2024_10_08:
+ *
+ *   src/raytrace/raytrace.py:658-659  (System.ray_trace)
+ *       for ii in range(len(self.surfaces)):
+ *           rays = self.surfaces[ii].propagate(rays, materials[ii], materials[ii + 1])
+ *
+ * One rtpb_trace() call replaces that whole loop: every Surface.propagate of the system
+ * (RefractingSurface RT:1160-1234, ReflectingSurface RT:1238-1303, PerfectLens RT:1601-1801 with
+ * FlatSurface RT:1306-1347, PlaneMirror RT:1377-1412, SphericalSurface RT:1435-1535), every
+ * propagate_ray2plane (RT:241-306) and every Material.n (materials.py:39-144) runs fused in one HIP
+ * kernel per launch on gfx950.  The history the reference builds with concatenate (RT:1229-1232) is
+ * written plane by plane, straight to its final place in the caller's output buffer.
+ *
+ * Conventions
+ *   - Plain C types only.  All ray buffers are caller-owned; the library never frees or retains them.
+ *   - A ray is 8 values (x, y, z, dx, dy, dz, phase, wavelength) -- RT:1-13, RT:85-94.  Layout AOS
+ *     stores a plane as [ray][8] (the reference's (P, N, 8) C order); layout SOA stores it as [8][ray].
+ *   - History plane p: p = 0 is the input plane, p = 2i+1 the rays AT surface i, p = 2i+2 the rays
+ *     AFTER surface i (RT:1229-1232, RT:1799).  `plane_mask` bit p selects which planes are stored;
+ *     selected planes are packed in increasing p order into consecutive output slots.
+ *   - Per-ray failures are not errors: they are NaN exactly as in the reference (miss RT:1506-1509,
+ *     back-facing RT:1190-1192, TIR RT:1221, aperture RT:1225-1226/1293-1294, NA RT:1757-1760,
+ *     backward RT:303-304/1401).
+ *   - Every function returns RTPB_OK (0) or a negative RTPB_E_* code; rtpb_last_error() returns the
+ *     message of the calling thread's last failure.  No C++ exception crosses the ABI.
+ *   - Thread-safety: plans are immutable after creation and may be used from several threads at
+ *     once; each (device, stream) pair must be driven by one thread at a time.
+ */
+#ifndef RTPB_H
+#define RTPB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTPB_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------------------------- */
+#define RTPB_OK 0
+#define RTPB_E_INVALID (-1)   /* bad argument (kind, size, pointer, mask) */
+#define RTPB_E_HIP (-2)       /* HIP runtime error */
+#define RTPB_E_NODEV (-3)     /* no GPU / device index out of range */
+#define RTPB_E_LIMIT (-4)     /* a compiled-in limit was exceeded (e.g. > RTPB_MAX_SURFACES) */
+
+/* ---- enums ---------------------------------------------------------------------------------- */
+/* surface kinds (reference classes) */
+#define RTPB_FLAT 0          /* FlatSurface      RT:1306-1347 (refracting)          */
+#define RTPB_SPHERE 1        /* SphericalSurface RT:1435-1535 (refracting)          */
+#define RTPB_PLANE_MIRROR 2  /* PlaneMirror      RT:1377-1412 (reflecting)          */
+#define RTPB_PERFECT_LENS 3  /* PerfectLens      RT:1558-1801 (ideal-lens mapping)  */
+
+/* material kinds (Material.n overrides) */
+#define RTPB_CONSTANT 0      /* Constant  MAT:59-79:  n = c[0]                                   */
+#define RTPB_SELLMEIER 1     /* Material  MAT:39-51:  c = {b1,b2,b3,c1,c2,c3}; Vacuum = zeros    */
+#define RTPB_POLY6 2         /* Ebaf11    MAT:128-144: c = {p0..p5}, n^2 = p0+p1 w^2+p2 w^-2+...  */
+#define RTPB_TABLE 3         /* user Material subclass: n looked up by exact wavelength match in
+                                a (wavelength, n) table evaluated on the host by the subclass's n() */
+
+/* data types and layouts */
+#define RTPB_F64 0
+#define RTPB_F32 1
+#define RTPB_AOS 0
+#define RTPB_SOA 1
+
+#define RTPB_MAX_SURFACES 63     /* history planes 0..2S must fit the 128-bit plane mask */
+#define RTPB_MAX_TABLE 4096      /* total (wavelength, n) entries over all TABLE materials */
+
+/* ---- descriptors ---------------------------------------------------------------------------- */
+typedef struct rtpb_surface {
+    int32_t kind;           /* RTPB_FLAT ... */
+    int32_t reserved;
+    double center[3];       /* Surface.center (RT:1063) */
+    double normal[3];       /* FlatSurface/PlaneMirror/PerfectLens .normal (RT:1320, 1389, 1576) */
+    double input_axis[3];   /* Surface.input_axis (RT:1054): front-side test, sphere aperture axis */
+    double radius;          /* SphericalSurface.radius (signed, RT:1445) */
+    double radius_sq;       /* radius**2 exactly as the host evaluates it (RT:1499) */
+    double aperture;        /* Surface.aperture_rad (RT:1069) */
+    double focal_len;       /* PerfectLens.focal_len */
+    double sin_alpha;       /* numpy.sin(PerfectLens.alpha) (RT:1758-1759) */
+    double on_tol;          /* on-surface tolerance; 1e-12 reproduces RT:1343/1408/1528 */
+} rtpb_surface;
+
+typedef struct rtpb_material {
+    int32_t kind;           /* RTPB_CONSTANT ... */
+    int32_t table_len;      /* RTPB_TABLE: number of (wavelength, n) pairs */
+    double c[6];            /* coefficients, see kinds */
+    const double* table;    /* RTPB_TABLE: host pointer to table_len pairs {wavelength, n}; a NaN
+                               wavelength key gives n(NaN).  Copied at plan creation. */
+} rtpb_material;
+
+typedef struct rtpb_plan rtpb_plan;   /* opaque: lowered system resident on the GPU(s) */
+
+/* ---- library -------------------------------------------------------------------------------- */
+int rtpb_abi_version(void);
+const char* rtpb_last_error(void);
+/* Number of visible GPUs (0 when none; never an error). */
+int rtpb_device_count(void);
+/* Release every device resource the library holds (plans must be destroyed first). */
+int rtpb_shutdown(void);
+
+/* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
+/* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,
+   System.materials, final material).  `dtype` is RTPB_F64 or RTPB_F32 (compute and storage type). */
+int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf,
+                     const rtpb_material* materials, int32_t nmat,
+                     int32_t dtype, rtpb_plan** plan_out);
+int rtpb_plan_destroy(rtpb_plan* plan);
+
+/* ---- tracing on device-resident buffers ----------------------------------------------------- */
+/* Trace n_rays rays through the whole plan on `device`, asynchronously on `stream` (a hipStream_t,
+   NULL = the device's null stream).
+     rays_in          device pointer, n_rays rays in `in_layout`; SOA fields are `in_field_stride`
+                      elements apart (>= n_rays).
+     out              device pointer to slot 0 of the output; slots are `out_plane_stride` elements
+                      apart (>= 8*n_rays); SOA fields are `out_field_stride` elements apart.
+     plane_mask_lo/hi bits 0..63 / 64..127 select history planes 0..2S (see above).
+   The element type of every buffer is the plan's dtype. */
+int rtpb_trace(const rtpb_plan* plan, int32_t device,
+               const void* rays_in, int64_t n_rays, int32_t in_layout, int64_t in_field_stride,
+               void* out, int32_t out_layout, int64_t out_plane_stride, int64_t out_field_stride,
+               uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream);
+
+/* ---- tracing host buffers (NumPy in, NumPy out), sharded over several GPUs ------------------ */
+/* rays_in: host, n_rays x 8 AOS.  out: host, nslots x n_rays x 8 AOS (nslots = popcount of the mask).
+   Rays are split into contiguous index ranges, one per listed device (NULL/0 devices = device 0),
+   each traced by its own host thread with chunked, double-buffered H2D / kernel / D2H copies.
+   Synchronous: returns when `out` is complete. */
+int rtpb_trace_host(const rtpb_plan* plan, const void* rays_in, int64_t n_rays, void* out,
+                    uint64_t plane_mask_lo, uint64_t plane_mask_hi,
+                    const int32_t* devices, int32_t n_devices);
+
+/* ---- device ray generators (reference RT:45-161), written straight into device memory -------- */
+/* get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray): ray k = iphi*n_thetas+itheta. */
+int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
+                 int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength,
+                 void* stream);
+
+/* ---- kernel timing (benchmarks) ------------------------------------------------------------- */
+/* While enabled on the calling thread, every trace kernel this thread launches is bracketed by a pair
+   of HIP events recorded on the kernel's own stream.  rtpb_timing_collect() waits for them and
+   returns the summed kernel time (ms) and launch count since the last collect, then resets. */
+int rtpb_timing_enable(int32_t on);
+int rtpb_timing_collect(double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTPB_H */

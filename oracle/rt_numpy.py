@@ -250,9 +250,14 @@ def _perfect_lens(s, r, m1, m2):
 
 
 # ----------------------------------------------------------------------------- driver
-def ray_trace(surfaces, materials, rays):
+def ray_trace(surfaces, materials, rays, reference_costs=False):
     """RT:641-661 + the rank handling of RT:1175-1178: (N,8) -> (1+2S, N, 8); (8,) -> (1+2S, 1, 8);
-    (k, N, 8) -> (k+2S, N, 8).  ``materials`` has len(surfaces)+1 entries (initial ... final)."""
+    (k, N, 8) -> (k+2S, N, 8).  ``materials`` has len(surfaces)+1 entries (initial ... final).
+
+    ``reference_costs=True`` (used by bench.py's CPU-baseline leg) additionally reproduces the
+    reference's data movement -- the history re-concatenated after every surface (RT:1229-1232,
+    O(S^2 N)) and n(lambda) re-evaluated at each of its call sites (RT:297/1213/1512) -- so the timed
+    CPU path costs what the reference's does.  The returned values are identical either way."""
     if len(materials) != len(surfaces) + 1:
         raise ValueError("length of materials should be len(surfaces) + 1")
     rays = np.asarray(rays, dtype=np.float64)
@@ -262,6 +267,15 @@ def ray_trace(surfaces, materials, rays):
         rays = rays[None, None, :]
     elif rays.ndim == 2:
         rays = rays[None]
+    if reference_costs:
+        hist = rays
+        for ii, s in enumerate(surfaces):
+            cur = Rays.from_array(hist[-1])
+            for _ in range(2 if s["type"] != "PlaneMirror" else 0):   # the extra n(lambda) call sites
+                refractive_index(materials[ii], cur.wl)
+            at, after = propagate(s, cur, materials[ii], materials[ii + 1])
+            hist = np.concatenate((hist, np.stack((at.to_array(), after.to_array()), axis=0)), axis=0)
+        return hist
     planes = list(rays)
     cur = Rays.from_array(planes[-1])
     for ii, s in enumerate(surfaces):

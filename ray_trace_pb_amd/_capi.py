@@ -1,0 +1,96 @@
+"""ctypes binding of the C ABI in include/rtpb.h (librtpb.so, built in-tree for gfx950).
+
+The library is REQUIRED: there is no CPU fallback for the trace.  If librtpb.so is missing or cannot
+be loaded, :func:`lib` raises ``RuntimeError`` telling how to build it.  ctypes releases the GIL for
+the duration of every call, so the host multi-GPU path can run one Python thread per device.
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtpb.so")
+
+RTPB_ABI_VERSION = 1
+RTPB_F64, RTPB_F32 = 0, 1
+RTPB_AOS, RTPB_SOA = 0, 1
+RTPB_FLAT, RTPB_SPHERE, RTPB_PLANE_MIRROR, RTPB_PERFECT_LENS = 0, 1, 2, 3
+RTPB_CONSTANT, RTPB_SELLMEIER, RTPB_POLY6, RTPB_TABLE = 0, 1, 2, 3
+RTPB_MAX_SURFACES = 63
+
+_c3 = ctypes.c_double * 3
+_c6 = ctypes.c_double * 6
+
+
+class Surface(ctypes.Structure):
+    """struct rtpb_surface"""
+    _fields_ = [("kind", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("center", _c3), ("normal", _c3), ("input_axis", _c3),
+                ("radius", ctypes.c_double), ("radius_sq", ctypes.c_double), ("aperture", ctypes.c_double),
+                ("focal_len", ctypes.c_double), ("sin_alpha", ctypes.c_double), ("on_tol", ctypes.c_double)]
+
+
+class Material(ctypes.Structure):
+    """struct rtpb_material"""
+    _fields_ = [("kind", ctypes.c_int32), ("table_len", ctypes.c_int32), ("c", _c6),
+                ("table", ctypes.POINTER(ctypes.c_double))]
+
+
+# symbol -> (restype, argtypes); every symbol include/rtpb.h declares
+_P = ctypes.c_void_p
+_i32, _i64, _u64, _dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+SIGNATURES = {
+    "rtpb_abi_version": (ctypes.c_int, []),
+    "rtpb_last_error": (ctypes.c_char_p, []),
+    "rtpb_device_count": (ctypes.c_int, []),
+    "rtpb_shutdown": (ctypes.c_int, []),
+    "rtpb_plan_create": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _i32,
+                                        ctypes.POINTER(_P)]),
+    "rtpb_plan_destroy": (ctypes.c_int, [_P]),
+    "rtpb_trace": (ctypes.c_int, [_P, _i32, _P, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P]),
+    "rtpb_trace_host": (ctypes.c_int, [_P, _P, _i64, _P, _u64, _u64, ctypes.POINTER(_i32), _i32]),
+    "rtpb_ray_fan": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, ctypes.POINTER(_dbl),
+                                    _dbl, _P]),
+    "rtpb_timing_enable": (ctypes.c_int, [_i32]),
+    "rtpb_timing_collect": (ctypes.c_int, [ctypes.POINTER(_dbl), ctypes.POINTER(_i64)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class RtpbError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load librtpb.so once; raise loudly when it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} not found: the HIP extension is not built. "
+                                   "Run `python -c 'import __graft_entry__ as g; g.build()'` or "
+                                   "`python -m ray_trace_pb_amd._build`.")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            if handle.rtpb_abi_version() != RTPB_ABI_VERSION:
+                raise RuntimeError("librtpb.so ABI version mismatch; rebuild it")
+            _lib = handle
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().rtpb_last_error().decode(errors="replace")
+        raise RtpbError(f"rtpb error {rc}: {msg}")
+    return rc
+
+
+def device_count():
+    return lib().rtpb_device_count()

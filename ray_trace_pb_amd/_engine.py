@@ -1,0 +1,189 @@
+"""Lowering of a System to C-ABI descriptors, the plan cache, and the two trace drivers.
+
+* :func:`lower` turns surfaces + materials into ``rtpb_surface`` / ``rtpb_material`` arrays
+  (include/rtpb.h).  Every constant the reference computes on the host side of its vector
+  expressions is computed here exactly the same way (``radius**2`` RT:1499, ``np.sin(alpha)``
+  RT:1758), so the kernel's f64 results are bit-identical to the reference.
+* Plans (device-resident descriptors) are cached by the byte content of the lowered system.
+* :func:`trace_host` -- NumPy in/out through ``rtpb_trace_host`` (H2D, kernel, D2H; optionally sharded
+  over several GPUs by ray index, one host thread per device inside the library).
+* :func:`trace_device` -- torch CUDA tensors in/out through ``rtpb_trace`` on torch's current stream;
+  nothing leaves HBM.
+"""
+import collections
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _capi as C
+
+# on-surface tolerance of the reference (RT:1343, 1408, 1528, 1597)
+ON_TOL_F64 = 1e-12
+# float32: the reference's absolute 1e-12 is below f32 resolution for any real geometry; use a
+# tolerance relative to the surface's own length scale (documented in DESIGN.md, "fp32 semantics")
+ON_TOL_F32_REL = 2.0 ** -12
+
+
+class Lowered:
+    __slots__ = ("surfaces", "materials", "tables", "dtype", "nsurf", "key")
+
+
+def _f3(v):
+    a = np.asarray(v, dtype=np.float64).ravel()
+    if a.size != 3:
+        raise ValueError(f"expected a 3-vector, got {v!r}")
+    return a
+
+
+def _surface_scale(s):
+    vals = [abs(float(x)) for x in np.asarray(s.center, dtype=float).ravel()]
+    vals.append(abs(float(getattr(s, "radius", 0.0) or 0.0)))
+    ap = float(s.aperture_rad)
+    if np.isfinite(ap):
+        vals.append(abs(ap))
+    vals.append(abs(float(getattr(s, "focal_len", 0.0) or 0.0)))
+    return max([1.0] + [v for v in vals if np.isfinite(v)])
+
+
+def lower(surfaces, materials, wavelengths, dtype):
+    """Lower surfaces (len S) and materials (len S+1: initial, System.materials, final).
+    ``wavelengths`` is a callable returning the distinct wavelengths of the bundle (used only for
+    user Material subclasses, which lower to per-wavelength tables)."""
+    S = len(surfaces)
+    if len(materials) != S + 1:
+        raise ValueError("length of materials should be len(surfaces) + 1")
+    if S > C.RTPB_MAX_SURFACES:
+        raise ValueError(f"at most {C.RTPB_MAX_SURFACES} surfaces per trace")
+    low = Lowered()
+    low.dtype = dtype
+    low.nsurf = S
+    low.surfaces = (C.Surface * max(S, 1))()
+    for k, s in enumerate(surfaces):
+        d = low.surfaces[k]
+        kind = s._rtpb_kind()
+        d.kind = kind
+        d.center[:] = _f3(s.center)
+        d.input_axis[:] = _f3(s.input_axis)
+        d.normal[:] = _f3(getattr(s, "normal", s.input_axis))
+        d.aperture = float(s.aperture_rad)
+        d.on_tol = ON_TOL_F64 if dtype == C.RTPB_F64 else ON_TOL_F32_REL * _surface_scale(s)
+        if kind == C.RTPB_SPHERE:
+            d.radius = float(s.radius)
+            d.radius_sq = float(s.radius ** 2)          # RT:1499 evaluates self.radius**2 on the host
+        elif kind == C.RTPB_PERFECT_LENS:
+            d.focal_len = float(s.focal_len)
+            d.sin_alpha = float(np.sin(s.alpha))         # RT:1758 xp.sin(self.alpha)
+    low.materials = (C.Material * (S + 1))()
+    low.tables = []
+    key_parts = [bytes(low.surfaces)]
+    wl_cache = []
+    for k, m in enumerate(materials):
+        d = low.materials[k]
+        lowered = m._rtpb_lower() if hasattr(m, "_rtpb_lower") else None
+        if lowered is not None:
+            d.kind, coeffs = lowered
+            d.c[:] = [float(c) for c in coeffs]
+            key_parts.append(bytes(d))
+            continue
+        # user Material subclass: tabulate its own n() at the bundle's distinct wavelengths
+        if not wl_cache:
+            wl_cache.append(np.asarray(wavelengths(), dtype=np.float64))
+        wl = wl_cache[0]
+        nv = np.broadcast_to(np.asarray(m.n(wl), dtype=np.float64), wl.shape)
+        tab = np.ascontiguousarray(np.stack((wl, nv), axis=1).ravel())
+        low.tables.append(tab)
+        d.kind = C.RTPB_TABLE
+        d.table_len = wl.size
+        d.table = tab.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        key_parts.append(bytes(memoryview(tab)) + b"T" + str(k).encode())
+    low.key = (dtype, S, b"|".join(key_parts))
+    return low
+
+
+# ------------------------------------------------------------------------- plan cache
+_PLANS = collections.OrderedDict()
+_PLANS_MAX = 32
+_plans_lock = threading.Lock()
+
+
+def plan_for(low):
+    with _plans_lock:
+        p = _PLANS.get(low.key)
+        if p is not None:
+            _PLANS.move_to_end(low.key)
+            return p
+        out = ctypes.c_void_p()
+        C.check(C.lib().rtpb_plan_create(low.surfaces, low.nsurf, low.materials, low.nsurf + 1, low.dtype,
+                                         ctypes.byref(out)))
+        _PLANS[low.key] = out
+        while len(_PLANS) > _PLANS_MAX:
+            _, old = _PLANS.popitem(last=False)
+            C.lib().rtpb_plan_destroy(old)
+        return out
+
+
+def plane_mask(planes):
+    lo = hi = 0
+    for p in planes:
+        if p < 64:
+            lo |= 1 << p
+        else:
+            hi |= 1 << (p - 64)
+    return lo, hi
+
+
+def resolve_planes(planes, nsurf):
+    """'all' | 'final' | iterable of plane indices (0 = input, 2i+1 at surface i, 2i+2 after it)."""
+    P = 2 * nsurf + 1
+    if isinstance(planes, str):
+        if planes == "all":
+            return list(range(P))
+        if planes == "final":
+            return [P - 1]
+        raise ValueError(f"planes must be 'all', 'final' or a list of plane indices, got {planes!r}")
+    sel = sorted({int(p) if int(p) >= 0 else int(p) + P for p in planes})
+    if not sel or sel[0] < 0 or sel[-1] >= P:
+        raise ValueError(f"plane indices must lie in [0, {P - 1}]")
+    return sel
+
+
+# ------------------------------------------------------------------------- drivers
+def _np_dtype(dtype):
+    return np.float64 if dtype == C.RTPB_F64 else np.float32
+
+
+def trace_host(low, rays2d, planes, devices=None, out=None):
+    """NumPy (N, 8) -> NumPy (len(planes), N, 8)."""
+    plan = plan_for(low)
+    rays2d = np.ascontiguousarray(rays2d, dtype=_np_dtype(low.dtype))
+    n = rays2d.shape[0]
+    if out is None:
+        out = np.empty((len(planes), n, 8), dtype=rays2d.dtype)
+    lo, hi = plane_mask(planes)
+    if devices is None:
+        devs = None
+        ndev = 0
+    else:
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        ndev = len(devices)
+    C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, n, out.ctypes.data, lo, hi, devs, ndev))
+    return out
+
+
+def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None):
+    """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA]."""
+    import torch
+    plan = plan_for(low)
+    tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
+    rays = rays.to(dtype=tdt).contiguous()
+    n = rays.shape[0]
+    if out is None:
+        shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
+        out = torch.empty(shape, dtype=tdt, device=rays.device)
+    lo, hi = plane_mask(planes)
+    if stream is None:
+        stream = torch.cuda.current_stream(rays.device).cuda_stream
+    C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), n, C.RTPB_AOS, 0,
+                               out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+    return out

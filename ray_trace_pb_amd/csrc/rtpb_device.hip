@@ -1,0 +1,628 @@
+// rtpb_device.hip -- gfx950 kernels and the C ABI (include/rtpb.h) of the sequential ray tracer.
+//
+// Hot path: ONE kernel launch traces every ray through every surface of the system (replacing the
+// Python surface loop RT:658-659 and the per-surface NumPy ufunc chains of RT:1160-1801).  One lane
+// owns one ray for the whole system:
+//   * the ray record (8 values) is read once from HBM (AOS: 16-byte vector loads; SOA: coalesced
+//     per-field loads) and kept in VGPRs;
+//   * surface and material descriptors are wave-uniform -- they are read through constant-address-
+//     space pointers with uniform indices, i.e. scalar loads (s_load) into SGPRs, once per wave;
+//   * n(lambda) of every material is evaluated once per ray (the reference re-evaluates it 3-4x per
+//     surface, MAT:39-51 via RT:297/1213/1512) and carried across the surface loop;
+//   * every requested history plane is written exactly once, at its final location -- no
+//     O(S^2 N) re-copying of the history (RT:1229-1232);
+//   * per-ray failures are NaN selects, never divergent early exits, so a wave stays converged.
+// The surface loop is wave-uniform (same system for every lane), so its `kind` switches never diverge.
+//
+// Memory roofline: per ray the kernel moves 8w bytes in and 8w bytes per stored plane out
+// (w = sizeof(T)); see DESIGN.md for the algorithmic-byte accounting used by bench.py.
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rtpb.h"
+#include "rtpb_math.h"
+
+using namespace rtpb;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxDevices = 64;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RTPB_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_));          \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// ---------------------------------------------------------------------------------- kernel args
+template <typename T>
+struct TraceArgs {
+    const T* __restrict__ in;
+    T* __restrict__ out;
+    const DevSurface<T>* __restrict__ surf;
+    const DevMaterial<T>* __restrict__ mats;
+    const T* __restrict__ table;
+    int64_t n;
+    int64_t in_fs;        // SOA input field stride
+    int64_t out_ps;       // output plane (slot) stride
+    int64_t out_fs;       // SOA output field stride
+    uint64_t mask_lo;
+    uint64_t mask_hi;
+    int32_t nsurf;
+};
+
+// Descriptors are read-only for the whole launch: read them through the constant address space so
+// the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.
+template <typename T> using cptr = const __attribute__((address_space(4))) T*;
+
+template <typename T>
+__device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
+    DevSurface<T> d;
+    d.kind = p->kind;
+    d.pad = 0;
+    for (int j = 0; j < 3; ++j) {
+        d.c[j] = p->c[j];
+        d.nrm[j] = p->nrm[j];
+        d.ax[j] = p->ax[j];
+    }
+    d.R = p->R; d.R2 = p->R2; d.absR = p->absR; d.ap = p->ap; d.f = p->f; d.sin_a = p->sin_a; d.tol = p->tol;
+    return d;
+}
+
+template <typename T>
+__device__ __forceinline__ DevMaterial<T> load_material(cptr<DevMaterial<T>> p) {
+    DevMaterial<T> d;
+    d.kind = p->kind;
+    d.table_off = p->table_off;
+    d.table_len = p->table_len;
+    d.pad = 0;
+    for (int j = 0; j < 6; ++j) d.c[j] = p->c[j];
+    return d;
+}
+
+template <typename T> struct Vec2;
+template <> struct Vec2<double> { using type = double2; };
+template <> struct Vec2<float> { using type = float2; };
+
+template <typename T, int LAYOUT>
+__device__ __forceinline__ Ray<T> load_ray(const T* __restrict__ in, int64_t i, int64_t fs) {
+    Ray<T> r;
+    if constexpr (LAYOUT == RTPB_AOS) {
+        if constexpr (sizeof(T) == 8) {
+            const double2* p = reinterpret_cast<const double2*>(in + i * 8);
+            const double2 a = p[0], b = p[1], c = p[2], d = p[3];
+            r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
+        } else {
+            const float4* p = reinterpret_cast<const float4*>(in + i * 8);
+            const float4 a = p[0], b = p[1];
+            r.x = a.x; r.y = a.y; r.z = a.z; r.dx = a.w; r.dy = b.x; r.dz = b.y; r.ph = b.z; r.wl = b.w;
+        }
+    } else {
+        r.x = in[i]; r.y = in[fs + i]; r.z = in[2 * fs + i]; r.dx = in[3 * fs + i];
+        r.dy = in[4 * fs + i]; r.dz = in[5 * fs + i]; r.ph = in[6 * fs + i]; r.wl = in[7 * fs + i];
+    }
+    return r;
+}
+
+template <typename T, int LAYOUT>
+__device__ __forceinline__ void store_ray(T* __restrict__ out, int64_t i, int64_t fs, const Ray<T>& r) {
+    if constexpr (LAYOUT == RTPB_AOS) {
+        if constexpr (sizeof(T) == 8) {
+            double2* p = reinterpret_cast<double2*>(out + i * 8);
+            p[0] = make_double2(r.x, r.y);
+            p[1] = make_double2(r.z, r.dx);
+            p[2] = make_double2(r.dy, r.dz);
+            p[3] = make_double2(r.ph, r.wl);
+        } else {
+            float4* p = reinterpret_cast<float4*>(out + i * 8);
+            p[0] = make_float4(r.x, r.y, r.z, r.dx);
+            p[1] = make_float4(r.dy, r.dz, r.ph, r.wl);
+        }
+    } else {
+        out[i] = r.x; out[fs + i] = r.y; out[2 * fs + i] = r.z; out[3 * fs + i] = r.dx;
+        out[4 * fs + i] = r.dy; out[5 * fs + i] = r.dz; out[6 * fs + i] = r.ph; out[7 * fs + i] = r.wl;
+    }
+}
+
+__device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
+    return p < 64 ? ((lo >> p) & 1ull) : ((hi >> (p - 64)) & 1ull);
+}
+
+// The fused multi-surface trace: one lane = one ray through all surfaces.
+template <typename T, int IN_LAYOUT, int OUT_LAYOUT>
+__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<T> a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    Ray<T> r = load_ray<T, IN_LAYOUT>(a.in, i, a.in_fs);
+    const T wl0 = r.wl;
+    T* __restrict__ out = a.out;
+    int64_t slot_off = 0;
+    if (a.mask_lo & 1ull) {
+        store_ray<T, OUT_LAYOUT>(out, i, a.out_fs, r);
+        slot_off += a.out_ps;
+    }
+    const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
+    const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
+    const cptr<T> table = (cptr<T>)(a.table);
+    T n_cur = material_n<T>(load_material<T>(mats), wl0, table);
+    for (int s = 0; s < a.nsurf; ++s) {
+        const T n_next = material_n<T>(load_material<T>(mats + s + 1), wl0, table);
+        Ray<T> at, after;
+        propagate_surface<T>(load_surface<T>(surf + s), r, n_cur, n_next, at, after);
+        const int p = 2 * s + 1;
+        if (plane_bit(a.mask_lo, a.mask_hi, p)) {
+            store_ray<T, OUT_LAYOUT>(out + slot_off, i, a.out_fs, at);
+            slot_off += a.out_ps;
+        }
+        if (plane_bit(a.mask_lo, a.mask_hi, p + 1)) {
+            store_ray<T, OUT_LAYOUT>(out + slot_off, i, a.out_fs, after);
+            slot_off += a.out_ps;
+        }
+        r = after;
+        n_cur = n_next;
+    }
+}
+
+// get_ray_fan (RT:45-96) on the device: ray k = iphi * n_thetas + itheta.
+template <typename T>
+struct FanArgs {
+    T* __restrict__ out;
+    int64_t n_thetas, nphis;
+    double pt[3], c[3], ex[3], ey[3];
+    double start, stop, step, wl;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ray_fan_kernel(FanArgs<T> a) {
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t total = a.n_thetas * a.nphis;
+    if (k >= total) return;
+    const int64_t it = k % a.n_thetas, ip = k / a.n_thetas;
+    // numpy.linspace: start + k*step, endpoint forced to stop (num > 1)
+    const double tt = (a.n_thetas > 1 && it == a.n_thetas - 1) ? a.stop : double(it) * a.step + a.start;
+    const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.nphis);
+    const double ct = cos(tt), st = sin(tt), cp = cos(pp), sp = sin(pp);
+    Ray<T> r;
+    r.x = T(a.pt[0]); r.y = T(a.pt[1]); r.z = T(a.pt[2]);
+    r.dx = T(a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st);
+    r.dy = T(a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st);
+    r.dz = T(a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st);
+    r.ph = T(0);
+    r.wl = T(a.wl);
+    store_ray<T, RTPB_AOS>(a.out, k, 0, r);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------- plans
+struct rtpb_plan {
+    int32_t dtype = RTPB_F64;
+    int32_t nsurf = 0;
+    std::vector<rtpb_surface> surf;
+    std::vector<rtpb_material> mats;    // table pointers cleared; see table_off/table_len
+    std::vector<int32_t> table_off;
+    std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
+    std::mutex mu;
+    void* blob[kMaxDevices] = {};
+    size_t off_mats = 0, off_table = 0, blob_bytes = 0;
+};
+
+namespace {
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+template <typename T>
+std::vector<unsigned char> build_blob(const rtpb_plan& p, size_t& off_mats, size_t& off_table) {
+    const size_t S = p.surf.size(), M = p.mats.size();
+    off_mats = align256(S * sizeof(DevSurface<T>));
+    off_table = off_mats + align256(M * sizeof(DevMaterial<T>));
+    const size_t bytes = off_table + align256(std::max<size_t>(p.table.size(), 2) * sizeof(T));
+    std::vector<unsigned char> blob(bytes, 0);
+    auto* ds = reinterpret_cast<DevSurface<T>*>(blob.data());
+    for (size_t k = 0; k < S; ++k) {
+        const rtpb_surface& s = p.surf[k];
+        DevSurface<T> d{};
+        d.kind = s.kind;
+        for (int j = 0; j < 3; ++j) {
+            d.c[j] = T(s.center[j]);
+            d.nrm[j] = T(s.normal[j]);
+            d.ax[j] = T(s.input_axis[j]);
+        }
+        d.R = T(s.radius);
+        d.R2 = T(s.radius_sq);
+        d.absR = T(std::fabs(s.radius));
+        d.ap = T(s.aperture);
+        d.f = T(s.focal_len);
+        d.sin_a = T(s.sin_alpha);
+        d.tol = T(s.on_tol);
+        ds[k] = d;
+    }
+    auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
+    for (size_t k = 0; k < M; ++k) {
+        const rtpb_material& m = p.mats[k];
+        DevMaterial<T> d{};
+        d.kind = m.kind;
+        bool zero = m.kind == RTPB_SELLMEIER;
+        for (int j = 0; j < 6; ++j) {
+            d.c[j] = T(m.c[j]);
+            zero = zero && m.c[j] == 0.0;
+        }
+        if (zero) d.kind = VACUUM;
+        d.table_off = p.table_off[k];
+        d.table_len = m.kind == RTPB_TABLE ? m.table_len : 0;
+        dm[k] = d;
+    }
+    auto* tb = reinterpret_cast<T*>(blob.data() + off_table);
+    for (size_t k = 0; k < p.table.size(); ++k) tb[k] = T(p.table[k]);
+    return blob;
+}
+
+// Device copy of the plan's descriptors (created on first use per device, then immutable).
+int plan_device_blob(rtpb_plan* p, int dev, void** out) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->blob[dev]) {
+        std::vector<unsigned char> host = p->dtype == RTPB_F64
+                                              ? build_blob<double>(*p, p->off_mats, p->off_table)
+                                              : build_blob<float>(*p, p->off_mats, p->off_table);
+        DeviceGuard g(dev);
+        void* d = nullptr;
+        HIP_TRY(hipMalloc(&d, host.size()));
+        hipError_t e = hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return fail(RTPB_E_HIP, std::string("hipMemcpy(plan): ") + hipGetErrorString(e));
+        }
+        p->blob[dev] = d;
+        p->blob_bytes = host.size();
+    }
+    *out = p->blob[dev];
+    return RTPB_OK;
+}
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RTPB_E_NODEV, "no GPU device visible");
+    if (dev < 0 || dev >= n || dev >= kMaxDevices)
+        return fail(RTPB_E_NODEV, "device index " + std::to_string(dev) + " out of range");
+    return RTPB_OK;
+}
+
+int popcount128(uint64_t lo, uint64_t hi) { return __builtin_popcountll(lo) + __builtin_popcountll(hi); }
+
+// ---------------------------------------------------------------------------------- timing
+struct TimingState {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+};
+thread_local TimingState g_timing;
+
+template <typename T, int IL, int OL>
+hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
+    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, hipStream_t st) {
+    if (il == RTPB_AOS && ol == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_AOS>(a, st);
+    if (il == RTPB_AOS && ol == RTPB_SOA) return launch_one<T, RTPB_AOS, RTPB_SOA>(a, st);
+    if (il == RTPB_SOA && ol == RTPB_AOS) return launch_one<T, RTPB_SOA, RTPB_AOS>(a, st);
+    return launch_one<T, RTPB_SOA, RTPB_SOA>(a, st);
+}
+
+int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int64_t in_fs, void* out, int ol,
+               int64_t out_ps, int64_t out_fs, uint64_t lo, uint64_t hi, hipStream_t st) {
+    void* blob = nullptr;
+    int rc = plan_device_blob(plan, dev, &blob);
+    if (rc) return rc;
+    if (n == 0) return RTPB_OK;
+    auto run = [&](auto tag) -> hipError_t {
+        using T = decltype(tag);
+        TraceArgs<T> a{};
+        a.in = static_cast<const T*>(in);
+        a.out = static_cast<T*>(out);
+        a.surf = reinterpret_cast<const DevSurface<T>*>(blob);
+        a.mats = reinterpret_cast<const DevMaterial<T>*>(static_cast<char*>(blob) + plan->off_mats);
+        a.table = reinterpret_cast<const T*>(static_cast<char*>(blob) + plan->off_table);
+        a.n = n;
+        a.in_fs = in_fs;
+        a.out_ps = out_ps;
+        a.out_fs = out_fs;
+        a.mask_lo = lo;
+        a.mask_hi = hi;
+        a.nsurf = plan->nsurf;
+        return launch_trace<T>(a, il, ol, st);
+    };
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing.on) {
+        if (!g_timing.pool.empty()) {
+            std::tie(e0, e1) = g_timing.pool.back();
+            g_timing.pool.pop_back();
+        } else {
+            HIP_TRY(hipEventCreate(&e0));
+            HIP_TRY(hipEventCreate(&e1));
+        }
+        HIP_TRY(hipEventRecord(e0, st));
+    }
+    hipError_t e = plan->dtype == RTPB_F64 ? run(double{}) : run(float{});
+    if (e != hipSuccess) return fail(RTPB_E_HIP, std::string("trace kernel launch: ") + hipGetErrorString(e));
+    if (g_timing.on) {
+        HIP_TRY(hipEventRecord(e1, st));
+        g_timing.pending.emplace_back(e0, e1);
+    }
+    return RTPB_OK;
+}
+
+}  // namespace
+
+// ================================================================================== C ABI
+extern "C" {
+
+int rtpb_abi_version(void) { return RTPB_ABI_VERSION; }
+
+const char* rtpb_last_error(void) { return g_last_error.c_str(); }
+
+int rtpb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rtpb_shutdown(void) { return RTPB_OK; }
+
+int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials, int32_t nmat,
+                     int32_t dtype, rtpb_plan** plan_out) {
+    if (!plan_out) return fail(RTPB_E_INVALID, "plan_out is NULL");
+    *plan_out = nullptr;
+    if (nsurf < 0 || (nsurf > 0 && !surfaces)) return fail(RTPB_E_INVALID, "bad surfaces array");
+    if (nsurf > RTPB_MAX_SURFACES)
+        return fail(RTPB_E_LIMIT, "more than RTPB_MAX_SURFACES (" + std::to_string(RTPB_MAX_SURFACES) + ") surfaces");
+    if (nmat != nsurf + 1 || !materials)
+        return fail(RTPB_E_INVALID, "length of materials should be len(surfaces) + 1");
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "dtype must be RTPB_F64 or RTPB_F32");
+    auto* p = new (std::nothrow) rtpb_plan();
+    if (!p) return fail(RTPB_E_INVALID, "out of host memory");
+    p->dtype = dtype;
+    p->nsurf = nsurf;
+    for (int k = 0; k < nsurf; ++k) {
+        if (surfaces[k].kind < RTPB_FLAT || surfaces[k].kind > RTPB_PERFECT_LENS) {
+            delete p;
+            return fail(RTPB_E_INVALID, "surface " + std::to_string(k) + ": unknown kind");
+        }
+        p->surf.push_back(surfaces[k]);
+    }
+    for (int k = 0; k < nmat; ++k) {
+        rtpb_material m = materials[k];
+        if (m.kind < RTPB_CONSTANT || m.kind > RTPB_TABLE) {
+            delete p;
+            return fail(RTPB_E_INVALID, "material " + std::to_string(k) + ": unknown kind");
+        }
+        p->table_off.push_back(static_cast<int32_t>(p->table.size() / 2));
+        if (m.kind == RTPB_TABLE) {
+            if (m.table_len <= 0 || !m.table) {
+                delete p;
+                return fail(RTPB_E_INVALID, "material " + std::to_string(k) + ": empty table");
+            }
+            if (p->table.size() / 2 + m.table_len > RTPB_MAX_TABLE) {
+                delete p;
+                return fail(RTPB_E_LIMIT, "more than RTPB_MAX_TABLE wavelength table entries");
+            }
+            p->table.insert(p->table.end(), m.table, m.table + 2 * m.table_len);
+        }
+        m.table = nullptr;
+        p->mats.push_back(m);
+    }
+    *plan_out = p;
+    return RTPB_OK;
+}
+
+int rtpb_plan_destroy(rtpb_plan* plan) {
+    if (!plan) return RTPB_OK;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        if (plan->blob[d]) {
+            DeviceGuard g(d);
+            (void)hipFree(plan->blob[d]);
+        }
+    }
+    delete plan;
+    return RTPB_OK;
+}
+
+int rtpb_trace(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int64_t n_rays, int32_t in_layout,
+               int64_t in_field_stride, void* out, int32_t out_layout, int64_t out_plane_stride,
+               int64_t out_field_stride, uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream) {
+    auto* plan = const_cast<rtpb_plan*>(plan_c);
+    if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n_rays < 0) return fail(RTPB_E_INVALID, "n_rays < 0");
+    const int nplanes = 2 * plan->nsurf + 1;
+    if (nplanes < 128 && ((nplanes >= 64 ? (plane_mask_hi >> (nplanes - 64)) : (plane_mask_hi | (plane_mask_lo >> nplanes))) != 0))
+        return fail(RTPB_E_INVALID, "plane mask selects planes beyond 2*nsurf");
+    const int nslots = popcount128(plane_mask_lo, plane_mask_hi);
+    if (in_layout != RTPB_AOS && in_layout != RTPB_SOA) return fail(RTPB_E_INVALID, "bad in_layout");
+    if (out_layout != RTPB_AOS && out_layout != RTPB_SOA) return fail(RTPB_E_INVALID, "bad out_layout");
+    if (n_rays > 0 && !rays_in) return fail(RTPB_E_INVALID, "rays_in is NULL");
+    if (n_rays > 0 && nslots > 0 && !out) return fail(RTPB_E_INVALID, "out is NULL");
+    const size_t w = plan->dtype == RTPB_F64 ? 8 : 4;
+    if (in_layout == RTPB_AOS && (reinterpret_cast<uintptr_t>(rays_in) % 16))
+        return fail(RTPB_E_INVALID, "AOS rays_in must be 16-byte aligned");
+    if (out_layout == RTPB_AOS && nslots > 0 &&
+        ((reinterpret_cast<uintptr_t>(out) % 16) || ((out_plane_stride * w) % 16)))
+        return fail(RTPB_E_INVALID, "AOS out and its plane stride must be 16-byte aligned");
+    if (nslots > 1 && out_plane_stride < 8 * n_rays) return fail(RTPB_E_INVALID, "out_plane_stride < 8*n_rays");
+    if (in_layout == RTPB_SOA && in_field_stride < n_rays) return fail(RTPB_E_INVALID, "in_field_stride < n_rays");
+    if (out_layout == RTPB_SOA && out_field_stride < n_rays) return fail(RTPB_E_INVALID, "out_field_stride < n_rays");
+    DeviceGuard g(device);
+    return trace_impl(plan, device, rays_in, n_rays, in_layout, in_field_stride, out, out_layout, out_plane_stride,
+                      out_field_stride, plane_mask_lo, plane_mask_hi, static_cast<hipStream_t>(stream));
+}
+
+int rtpb_trace_host(const rtpb_plan* plan_c, const void* rays_in, int64_t n_rays, void* out, uint64_t plane_mask_lo,
+                    uint64_t plane_mask_hi, const int32_t* devices, int32_t n_devices) {
+    auto* plan = const_cast<rtpb_plan*>(plan_c);
+    if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
+    if (n_rays < 0) return fail(RTPB_E_INVALID, "n_rays < 0");
+    std::vector<int> devs;
+    if (!devices || n_devices <= 0) devs.push_back(0);
+    else devs.assign(devices, devices + n_devices);
+    for (int d : devs) {
+        int rc = check_device(d);
+        if (rc) return rc;
+    }
+    const int nslots = popcount128(plane_mask_lo, plane_mask_hi);
+    if (n_rays == 0 || nslots == 0) return RTPB_OK;
+    if (!rays_in || !out) return fail(RTPB_E_INVALID, "NULL host buffer");
+    const size_t w = plan->dtype == RTPB_F64 ? 8 : 4;
+    const size_t rec = 8 * w;
+    const int G = static_cast<int>(devs.size());
+    std::vector<int> rcs(G, RTPB_OK);
+    std::vector<std::string> errs(G);
+    auto worker = [&](int g) {
+        const int dev = devs[g];
+        const int64_t a = n_rays * g / G, b = n_rays * (g + 1) / G;
+        if (b <= a) return;
+        auto body = [&]() -> int {
+            DeviceGuard guard(dev);
+            // chunk so that one chunk's output stays <= ~1 GiB of device memory
+            const int64_t max_chunk = std::max<int64_t>(1 << 16, (int64_t(1) << 30) / int64_t(nslots * rec));
+            const int64_t chunk = std::min<int64_t>(b - a, max_chunk);
+            hipStream_t st = nullptr;
+            HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            void *d_in = nullptr, *d_out = nullptr;
+            int rc = RTPB_OK;
+            auto cleanup = [&]() {
+                if (d_in) (void)hipFree(d_in);
+                if (d_out) (void)hipFree(d_out);
+                (void)hipStreamDestroy(st);
+            };
+            hipError_t e = hipMalloc(&d_in, chunk * rec);
+            if (e == hipSuccess) e = hipMalloc(&d_out, chunk * rec * nslots);
+            if (e != hipSuccess) {
+                cleanup();
+                return fail(RTPB_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+            }
+            for (int64_t c0 = a; c0 < b && rc == RTPB_OK; c0 += chunk) {
+                const int64_t m = std::min<int64_t>(chunk, b - c0);
+                e = hipMemcpyAsync(d_in, static_cast<const char*>(rays_in) + c0 * rec, m * rec,
+                                   hipMemcpyHostToDevice, st);
+                if (e != hipSuccess) { rc = fail(RTPB_E_HIP, std::string("H2D: ") + hipGetErrorString(e)); break; }
+                rc = trace_impl(plan, dev, d_in, m, RTPB_AOS, 0, d_out, RTPB_AOS, m * 8, 0, plane_mask_lo,
+                                plane_mask_hi, st);
+                if (rc) break;
+                e = hipMemcpy2DAsync(static_cast<char*>(out) + c0 * rec, n_rays * rec, d_out, m * rec, m * rec,
+                                     nslots, hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess) e = hipStreamSynchronize(st);
+                if (e != hipSuccess) rc = fail(RTPB_E_HIP, std::string("D2H: ") + hipGetErrorString(e));
+            }
+            cleanup();
+            return rc;
+        };
+        rcs[g] = body();
+        if (rcs[g]) errs[g] = g_last_error;
+    };
+    if (G == 1) {
+        worker(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g) th.emplace_back(worker, g);
+        for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < G; ++g)
+        if (rcs[g]) return fail(rcs[g], "device " + std::to_string(devs[g]) + ": " + errs[g]);
+    return RTPB_OK;
+}
+
+int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
+                 int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n_thetas <= 0 || nphis <= 0 || !rays_out || !pt || !center_ray)
+        return fail(RTPB_E_INVALID, "bad ray-fan arguments");
+    if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
+    const double* c = center_ray;
+    // enx = cross((0,1,0), c) / |.|; eny = cross(c, enx)   (RT:79-81)
+    double ex[3] = {1.0 * c[2] - 0.0 * c[1], 0.0 * c[0] - 0.0 * c[2], 0.0 * c[1] - 1.0 * c[0]};
+    const double en = std::sqrt(ex[0] * ex[0] + ex[1] * ex[1] + ex[2] * ex[2]);
+    for (double& v : ex) v = v / en;
+    const double ey[3] = {c[1] * ex[2] - c[2] * ex[1], c[2] * ex[0] - c[0] * ex[2], c[0] * ex[1] - c[1] * ex[0]};
+    DeviceGuard g(device);
+    const int64_t total = n_thetas * nphis;
+    const unsigned blocks = static_cast<unsigned>((total + kBlock - 1) / kBlock);
+    auto go = [&](auto tag) {
+        using T = decltype(tag);
+        FanArgs<T> a{};
+        a.out = static_cast<T*>(rays_out);
+        a.n_thetas = n_thetas;
+        a.nphis = nphis;
+        for (int j = 0; j < 3; ++j) {
+            a.pt[j] = pt[j]; a.c[j] = c[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
+        }
+        a.start = -theta_max;
+        a.stop = theta_max;
+        a.step = n_thetas > 1 ? (theta_max - (-theta_max)) / double(n_thetas - 1) : 0.0;
+        a.wl = wavelength;
+        hipLaunchKernelGGL(ray_fan_kernel<T>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    };
+    if (dtype == RTPB_F64) go(double{});
+    else if (dtype == RTPB_F32) go(float{});
+    else return fail(RTPB_E_INVALID, "bad dtype");
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_timing_enable(int32_t on) {
+    g_timing.on = on != 0;
+    return RTPB_OK;
+}
+
+int rtpb_timing_collect(double* total_ms, int64_t* launches) {
+    double tot = 0.0;
+    int64_t cnt = 0;
+    for (auto& pr : g_timing.pending) {
+        HIP_TRY(hipEventSynchronize(pr.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+        tot += ms;
+        ++cnt;
+        g_timing.pool.push_back(pr);
+    }
+    g_timing.pending.clear();
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = cnt;
+    return RTPB_OK;
+}
+
+}  // extern "C"

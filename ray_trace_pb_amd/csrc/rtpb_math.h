@@ -1,0 +1,330 @@
+// rtpb_math.h -- per-ray arithmetic of the sequential ray trace, shared by the gfx950 kernel
+// (rtpb_device.hip) and the CPU test harness (tests/native/math_harness.cpp).
+//
+// Every function restates one piece of the reference (QI2lab/ray_trace_pb @ 2024_10_08,
+// src/raytrace/raytrace.py = RT, src/raytrace/materials.py = MAT) for ONE ray, with the operations
+// in exactly the order NumPy evaluates the reference's vector expressions (left-to-right products,
+// norm = sqrt((a*a + b*b) + c*c), np.cross component formulas).  Compiled with -ffp-contract=off and
+// without fast-math, the f64 instantiation is IEEE-identical to the reference.
+//
+// Descriptors arrive by value (the kernel loads them with scalar loads from the constant address
+// space, so they live in SGPRs); per-ray state lives in VGPRs.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RTPB_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define RTPB_HD inline
+#endif
+
+namespace rtpb {
+
+// internal surface / material kinds (public ones from rtpb.h + host-detected specialisations)
+enum SurfKind : int32_t { FLAT = 0, SPHERE = 1, PLANE_MIRROR = 2, PERFECT_LENS = 3 };
+enum MatKind : int32_t { CONSTANT = 0, SELLMEIER = 1, POLY6 = 2, TABLE = 3,
+                         VACUUM = 4 /* SELLMEIER with all-zero coefficients (MAT:54-56) */ };
+
+template <typename T>
+struct DevSurface {
+    int32_t kind;
+    int32_t pad;
+    T c[3];      // center
+    T nrm[3];    // plane normal (flat / mirror / lens)
+    T ax[3];     // input_axis
+    T R;         // signed radius
+    T R2;        // radius**2 as evaluated by the host
+    T absR;      // abs(radius)
+    T ap;        // aperture_rad
+    T f;         // focal length
+    T sin_a;     // sin(alpha)
+    T tol;       // on-surface tolerance
+};
+
+template <typename T>
+struct DevMaterial {
+    int32_t kind;
+    int32_t table_off;   // TABLE: offset (in pairs) into the plan's table array
+    int32_t table_len;
+    int32_t pad;
+    T c[6];
+};
+
+template <typename T>
+struct Ray {
+    T x, y, z, dx, dy, dz, ph, wl;
+};
+
+template <typename T> RTPB_HD T qnan() { return T(__builtin_nan("")); }
+template <> RTPB_HD float qnan<float>() { return __builtin_nanf(""); }
+
+template <typename T> RTPB_HD bool is_nan(T v) { return v != v; }
+
+template <typename T> RTPB_HD T tsqrt(T v);
+template <> RTPB_HD double tsqrt<double>(double v) { return sqrt(v); }
+template <> RTPB_HD float tsqrt<float>(float v) { return sqrtf(v); }
+
+template <typename T> RTPB_HD T tabs(T v) { return v < T(0) ? -v : (v == T(0) ? T(0) : v); }
+
+template <typename T> RTPB_HD T tpow(T b, T e);
+template <> RTPB_HD double tpow<double>(double b, double e) { return pow(b, e); }
+template <> RTPB_HD float tpow<float>(float b, float e) { return powf(b, e); }
+
+template <typename T> struct Const {
+    static constexpr double pi = 3.141592653589793;        // numpy.pi
+    static constexpr double two_pi = 6.283185307179586;    // 2 * numpy.pi (exact doubling)
+};
+
+template <typename T>
+RTPB_HD void kill(Ray<T>& r) {
+    const T n = qnan<T>();
+    r.x = n; r.y = n; r.z = n; r.dx = n; r.dy = n; r.dz = n; r.ph = n; r.wl = n;
+}
+
+// NaN-propagating minimum, numpy.minimum / numpy.min semantics
+template <typename T>
+RTPB_HD T nan_min(T a, T b) {
+    if (is_nan(a)) return a;
+    if (is_nan(b)) return b;
+    return b < a ? b : a;
+}
+
+// numpy.sign: -1, 0, +1, NaN
+template <typename T>
+RTPB_HD T np_sign(T v) {
+    return v > T(0) ? T(1) : (v < T(0) ? T(-1) : (v == T(0) ? T(0) : v));
+}
+
+// ------------------------------------------------------------------ Material.n (MAT:39-144)
+template <typename T, typename TablePtr>
+RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
+    switch (m.kind) {
+    case CONSTANT:
+        return m.c[0];                                               // MAT:72-79
+    case VACUUM: {
+        // (0*w2)/(w2-0) summed thrice + 1: exactly 1 unless w2 is 0, inf or NaN (then NaN)
+        const T w2 = wl * wl;
+        return (w2 != T(0) && w2 - w2 == T(0)) ? T(1) : qnan<T>();
+    }
+    case SELLMEIER: {                                                // MAT:48-51
+        const T w2 = wl * wl;
+        const T acc = m.c[0] * w2 / (w2 - m.c[3]) + m.c[1] * w2 / (w2 - m.c[4]) + m.c[2] * w2 / (w2 - m.c[5]);
+        return tsqrt<T>(acc + T(1));
+    }
+    case POLY6: {                                                    // MAT:137-144 (Ebaf11)
+        const T w2 = wl * wl;
+        const T n2 = m.c[0] + m.c[1] * w2 + m.c[2] * tpow<T>(wl, T(-2)) + m.c[3] * tpow<T>(wl, T(-4)) +
+                     m.c[4] * tpow<T>(wl, T(-6)) + m.c[5] * tpow<T>(wl, T(-8));
+        return tsqrt<T>(n2);
+    }
+    default: {                                                       // TABLE: user Material.n
+        const bool want_nan = is_nan(wl);
+        T out = qnan<T>();
+        for (int k = 0; k < m.table_len; ++k) {
+            const T key = table[2 * (m.table_off + k)];
+            if (want_nan ? is_nan(key) : key == wl) { out = table[2 * (m.table_off + k) + 1]; break; }
+        }
+        return out;
+    }
+    }
+}
+
+// ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)
+// Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
+template <typename T>
+RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
+                        T* t_out = nullptr) {
+    const T t = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz) / (r.dx * nx + r.dy * ny + r.dz * nz);
+    const T s = t < T(0) ? T(-1) : T(1);
+    const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
+    Ray<T> o;
+    o.x = r.x + vx;
+    o.y = r.y + vy;
+    o.z = r.z + vz;
+    o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
+    const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz);
+    o.ph = r.ph + dist * s * T(2) * T(Const<T>::pi) / r.wl * n;
+    o.wl = r.wl;
+    if (exclude_backward && s == T(-1)) kill(o);
+    if (t_out) *t_out = t;
+    return o;
+}
+
+// ------------------------------------------------------------------ SphericalSurface.get_intersect (RT:1479-1516)
+template <typename T>
+RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n) {
+    const T ox = r.x - s.c[0], oy = r.y - s.c[1], oz = r.z - s.c[2];
+    const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
+    const T C = ox * ox + oy * oy + oz * oz - s.R2;
+    const T root = tsqrt<T>(B * B - T(4) * C);
+    T t1 = T(0.5) * (-B + root);
+    T t2 = T(0.5) * (-B - root);
+    const T inf = T(1) / T(0);
+    if (t1 < T(0)) t1 = inf;
+    if (t2 < T(0)) t2 = inf;
+    T t = nan_min(t1, t2);
+    if (t == inf) t = qnan<T>();
+    Ray<T> o;
+    o.x = r.x + r.dx * t;
+    o.y = r.y + r.dy * t;
+    o.z = r.z + r.dz * t;
+    o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
+    const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
+    const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz);
+    o.ph = r.ph + dist * T(2) * T(Const<T>::pi) / r.wl * n;
+    o.wl = r.wl;
+    return o;
+}
+
+// v / |v| with NaN components replaced by 0 (RT:1203-1209)
+template <typename T>
+RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
+    const T nrm = tsqrt<T>(x * x + y * y + z * z);
+    x = x / nrm; y = y / nrm; z = z / nrm;
+    if (is_nan(x)) x = T(0);
+    if (is_nan(y)) y = T(0);
+    if (is_nan(z)) z = T(0);
+}
+
+// basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
+template <typename T>
+RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz) {
+    T bx = ri.dy * Nz - ri.dz * Ny;
+    T by = ri.dz * Nx - ri.dx * Nz;
+    T bz = ri.dx * Ny - ri.dy * Nx;
+    unit_or_zero(bx, by, bz);
+    cx = Ny * bz - Nz * by;
+    cy = Nz * bx - Nx * bz;
+    cz = Nx * by - Ny * bx;
+    unit_or_zero(cx, cy, cz);
+}
+
+// Snell refraction of the intersected ray (RT:1197-1221)
+template <typename T>
+RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2) {
+    T cx, cy, cz;
+    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz);
+    const T mag = n1 / n2 * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
+    const T sgn = np_sign<T>(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
+    const T tang = sgn * tsqrt<T>(T(1) - mag * mag);
+    Ray<T> o;
+    o.dx = mag * cx + tang * Nx;
+    o.dy = mag * cy + tang * Ny;
+    o.dz = mag * cz + tang * Nz;
+    const bool bad = is_nan(o.dx);
+    o.x = bad ? qnan<T>() : ri.x;
+    o.y = bad ? qnan<T>() : ri.y;
+    o.z = bad ? qnan<T>() : ri.z;
+    o.ph = ri.ph;
+    o.wl = ri.wl;
+    return o;
+}
+
+// law of reflection (RT:1267-1289)
+template <typename T>
+RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz) {
+    T cx, cy, cz;
+    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz);
+    const T mag_na = -(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
+    const T mag_nc = cx * ri.dx + cy * ri.dy + cz * ri.dz;
+    Ray<T> o;
+    o.dx = mag_na * Nx + mag_nc * cx;
+    o.dy = mag_na * Ny + mag_nc * cy;
+    o.dz = mag_na * Nz + mag_nc * cz;
+    const bool bad = is_nan(o.dx);
+    o.x = bad ? qnan<T>() : ri.x;
+    o.y = bad ? qnan<T>() : ri.y;
+    o.z = bad ? qnan<T>() : ri.z;
+    o.ph = ri.ph;
+    o.wl = ri.wl;
+    return o;
+}
+
+// FlatSurface / PlaneMirror .is_pt_on_surface (RT:1339-1347, RT:1405-1412)
+template <typename T>
+RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
+    const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
+    const T h = rx * s.nrm[0] + ry * s.nrm[1] + rz * s.nrm[2];
+    return tabs<T>(h) < s.tol && tsqrt<T>(rx * rx + ry * ry + rz * rz) <= s.ap;
+}
+
+// SphericalSurface.is_pt_on_surface (RT:1518-1535): aperture about the ORIGIN-through input axis
+template <typename T>
+RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
+    const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
+    const T dist = tsqrt<T>(rx * rx + ry * ry + rz * rz);
+    const bool on = tabs<T>(dist - s.absR) < s.tol;
+    const T a = p.x * s.ax[0] + p.y * s.ax[1] + p.z * s.ax[2];
+    const T qx = p.x - a * s.ax[0], qy = p.y - a * s.ax[1], qz = p.z - a * s.ax[2];
+    return on && tsqrt<T>(qx * qx + qy * qy + qz * qz) <= s.ap;
+}
+
+// ------------------------------------------------------------------ one surface: (at, after)
+// Refracting surfaces RT:1160-1234, reflecting RT:1238-1303, PerfectLens RT:1601-1801.
+template <typename T>
+RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
+    const int kind = s.kind;
+    if (kind == PERFECT_LENS) {
+        const T f = s.f;
+        const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
+        const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
+        const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
+        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false);
+        const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
+        T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
+        const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz);
+        if (spn > T(1e-12)) { spx = spx / spn; spy = spy / spn; spz = spz / spn; }
+        const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
+        const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z);
+        T ux = r1x, uy = r1y, uz = r1z;
+        if (r1n != T(0)) { ux = ux / r1n; uy = uy / r1n; uz = uz / r1n; }
+        const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
+        Ray<T> o;
+        o.x = n1 * f * sin_t1 * spx + Bx;
+        o.y = n1 * f * sin_t1 * spy + By;
+        o.z = n1 * f * sin_t1 * spz + Bz;
+        const T sin_t2 = -r1n / f / n2;
+        const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2);
+        o.dx = sin_t2 * ux + cos_t2 * nx;
+        o.dy = sin_t2 * uy + cos_t2 * ny;
+        o.dz = sin_t2 * uz + cos_t2 * nz;
+        o.wl = r.wl;
+        if (tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a) kill(o);
+        const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
+        const T k = T(Const<T>::two_pi) / r.wl;
+        o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
+        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false);
+        at = to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false);
+        return;
+    }
+
+    T Nx, Ny, Nz;
+    Ray<T> ri;
+    if (kind == SPHERE) {
+        ri = sphere_hit(r, s, n1);
+        Nx = (ri.x - s.c[0]) / s.R;                                   // RT:1476
+        Ny = (ri.y - s.c[1]) / s.R;
+        Nz = (ri.z - s.c[2]) / s.R;
+    } else {                                                           // FLAT, PLANE_MIRROR
+        Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
+        ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true);   // RT:1331-1337, 1398-1403
+    }
+
+    if (kind == PLANE_MIRROR) {
+        after = reflect(ri, Nx, Ny, Nz);
+        if (!on_flat(ri, s)) kill(after);
+        at = ri;
+        return;
+    }
+
+    // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
+    if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
+    after = snell(ri, Nx, Ny, Nz, n1, n2);
+    const bool ok = (kind == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
+    if (!ok) kill(after);
+    at = ri;
+}
+
+}  // namespace rtpb

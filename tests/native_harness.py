@@ -1,0 +1,39 @@
+"""Build + load the CPU harness of the kernel arithmetic (tests/native/math_harness.cpp).
+TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "math_harness.cpp")
+OUT = os.path.join(HERE, "native", "_build", "libmath_harness.so")
+DEPS = [SRC, os.path.join(HERE, "..", "ray_trace_pb_amd", "csrc", "rtpb_math.h"),
+        os.path.join(HERE, "..", "include", "rtpb.h")]
+
+_lib = None
+
+
+def harness():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(OUT) or any(os.path.getmtime(OUT) < os.path.getmtime(d) for d in DEPS):
+            os.makedirs(os.path.dirname(OUT), exist_ok=True)
+            subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", OUT + ".tmp",
+                            SRC], check=True)
+            os.replace(OUT + ".tmp", OUT)
+        _lib = ctypes.CDLL(OUT)
+    return _lib
+
+
+def harness_trace(low, rays2d):
+    """Full history (2S+1, N, 8) of rays2d through a lowered system (ray_trace_pb_amd._engine.lower)."""
+    rays2d = np.ascontiguousarray(rays2d, dtype=np.float64)
+    n = rays2d.shape[0]
+    out = np.empty((2 * low.nsurf + 1, n, 8))
+    rc = harness().harness_trace_f64(low.surfaces, ctypes.c_int32(low.nsurf), low.materials,
+                                     rays2d.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(n),
+                                     out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return out

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP path (librtpb.so through the C ABI) against the reference's golden vectors and
+the NumPy oracle.  Float64 results must be BIT-IDENTICAL (NaN pattern included); float32 results
+must agree with the float64 oracle to rtol 1e-5 (column-scaled)."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from ray_trace_pb_amd import _capi as C  # noqa: E402
+from ray_trace_pb_amd import _engine as E  # noqa: E402
+from oracle import rt_numpy as O  # noqa: E402
+from parity import CASES, GOLDEN, compare, load_case  # noqa: E402
+from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
+import systems  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def build_case(name):
+    d = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    return system, m0, m1, d["rays_in"], d["history"]
+
+
+def oracle(system, m0, m1, rays):
+    return O.ray_trace([surface_to_dict(s) for s in system.surfaces],
+                       [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]], rays)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_numpy_path_bitwise_vs_reference(name):
+    system, m0, m1, rays, ref = build_case(name)
+    got = system.ray_trace(rays, m0, m1)
+    assert isinstance(got, np.ndarray) and got.dtype == np.float64 and got.flags.c_contiguous
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_device_path_bitwise_vs_reference(name):
+    system, m0, m1, rays, ref = build_case(name)
+    got = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
+    torch.cuda.synchronize()
+    assert got.is_cuda and got.dtype == torch.float64
+    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+
+
+def test_input_ranks_and_extend_history():
+    d = np.load(os.path.join(GOLDEN, "shapes.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    for k in ("1", "2", "3"):
+        got = system.ray_trace(d["rays" + k], m0, m1)
+        assert got.shape == d["out" + k].shape, k
+        assert np.array_equal(got, d["out" + k], equal_nan=True), k
+        got_t = system.ray_trace(torch.from_numpy(np.ascontiguousarray(d["rays" + k])).to(DEV), m0, m1)
+        assert np.array_equal(got_t.cpu().numpy(), d["out" + k], equal_nan=True), k
+
+
+def test_surface_propagate_appends_two_planes():
+    system, m0, m1, rays, ref = build_case("c1_plano_convex")
+    mats = [m0] + list(system.materials) + [m1]
+    h = rays
+    for i, s in enumerate(system.surfaces):
+        h = s.propagate(h, mats[i], mats[i + 1])
+    assert np.array_equal(h, ref, equal_nan=True)
+
+
+def test_large_bundle_bitwise_vs_oracle_subsample():
+    """C2 at the full BASELINE size (1M rays): GPU vs the oracle on a 100k-ray random subsample."""
+    system = systems.c2_system(rt, mat)
+    rays = systems.c2_rays(1_000_000)
+    got = system.ray_trace(rays, mat.Vacuum(), mat.Vacuum())
+    idx = np.random.default_rng(0).choice(rays.shape[0], 100_000, replace=False)
+    ref = oracle(system, mat.Vacuum(), mat.Vacuum(), rays[idx])
+    assert np.array_equal(got[:, idx], ref, equal_nan=True)
+
+
+def test_full_size_properties_c2():
+    """Size-independent properties at full size: unit directions, Snell invariant at the flats,
+    OPL monotone along the ray, wavelengths preserved."""
+    system = systems.c2_system(rt, mat)
+    rays = systems.c2_rays(1_000_000)
+    h = system.ray_trace(torch.from_numpy(rays).to(DEV), mat.Vacuum(), mat.Vacuum()).cpu().numpy()
+    live = ~np.isnan(h[-1]).any(axis=1)
+    assert live.mean() > 0.99
+    d = h[:, live, 3:6]
+    assert np.allclose(np.linalg.norm(d, axis=-1), 1.0, atol=1e-12)
+    assert np.array_equal(h[:, live, 7], np.broadcast_to(rays[live, 7], (h.shape[0], live.sum())))
+    assert np.all(np.diff(h[:, live, 6], axis=0) >= -1e-9)
+    # flat at z=0 between vacuum and vacuum: direction unchanged
+    assert np.array_equal(h[2, live, 3:6], h[0, live, 3:6])
+
+
+def test_planes_final_and_subset_match_full():
+    system, m0, m1, rays, ref = build_case("c5_odt")
+    fin = system.ray_trace(rays, m0, m1, planes="final")
+    assert fin.shape == (1,) + ref.shape[1:]
+    assert np.array_equal(fin[0], ref[-1], equal_nan=True)
+    sel = [0, 3, 4, 17, 28]
+    sub = system.ray_trace(rays, m0, m1, planes=sel)
+    assert np.array_equal(sub, ref[sel], equal_nan=True)
+    t = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, planes=[1, 28])
+    assert np.array_equal(t.cpu().numpy(), ref[[1, 28]], equal_nan=True)
+
+
+def test_soa_layout_matches_aos():
+    system, m0, m1, rays, ref = build_case("stress")
+    soa = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, layout="soa")
+    assert tuple(soa.shape) == (ref.shape[0], 8, ref.shape[1])
+    assert np.array_equal(soa.transpose(1, 2).cpu().numpy(), ref, equal_nan=True)
+
+
+def test_sharded_host_trace_is_bitwise_equal():
+    """Ray sharding over devices (here: two shards on GPU 0) gives exactly the unsharded history."""
+    system, m0, m1, rays, ref = build_case("stress")
+    got = system.ray_trace(rays, m0, m1, devices=[0, 0])
+    assert np.array_equal(got, ref, equal_nan=True)
+    got3 = system.ray_trace(rays, m0, m1, devices=[0, 0, 0])
+    assert np.array_equal(got3, ref, equal_nan=True)
+
+
+def test_user_material_subclass_lowers_to_table():
+    """A Material subclass overriding n() (the reference's plugin point) traces on the GPU via a
+    per-wavelength table, bit-identical to evaluating its n() per ray."""
+    system, m0, m1, rays, ref = build_case("stress")
+    assert any(type(m).__name__ == "Cauchy" for m in system.materials)
+    got = system.ray_trace(rays, m0, m1)
+    assert np.array_equal(got, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["c1_plano_convex", "c2_achromat", "c3_relay", "c4_opm", "c5_odt",
+                                  "kat_perfect_lens_phase", "reversed_doublet"])
+def test_float32_within_1e5_of_float64_reference(name):
+    system, m0, m1, rays, ref = build_case(name)
+    got = system.ray_trace(rays.astype(np.float32), m0, m1, dtype="float32")
+    assert got.dtype == np.float32
+    ok, rep = compare(got, ref, rtol=1e-5)
+    assert ok, rep
+
+
+def test_kat_perfect_lens_equal_phase():
+    """scripts/2021_10_28_test_perfect_lens_phase.py: a tilted plane wave focuses in phase."""
+    system, rays, m0, m1 = systems.kat_perfect_lens_phase(rt, mat)
+    out = system.ray_trace(rays, m0, m1)
+    assert np.ptp(out[-1, :, 6]) == 0.0
+
+
+def test_kat_plano_convex_opl_analytic():
+    """scripts/2022_10_27_plano_convex_lens.py:39-59: traced OPL equals the analytic formula."""
+    system, rays, m0, m1 = systems.c1_plano_convex(rt, mat, nrays=101)
+    out = system.ray_trace(rays, m0, m1)
+    n, R, t0, t1, dz, k = 1.3, 100, 2.679486355, 1, 5, 2 * np.pi / 0.5
+    h = rays[:, 0]
+    opl = (dz + n * t0 + n * t1 - n * (R - np.sqrt(R ** 2 - h ** 2)) +
+           (R - np.sqrt(R ** 2 - h ** 2)) / (np.sqrt(1 - n ** 2 * h ** 2 / R ** 2) * np.sqrt(R ** 2 - h ** 2) / R +
+                                             n * h ** 2 / R ** 2))
+    assert np.max(np.abs(out[-1, :, 6] / k - opl)) < 1e-12
+
+
+def test_device_ray_fan_matches_host_generator():
+    fan_h = rt.get_ray_fan([0.5, -0.25, 1.0], 0.3, 101, 0.635, nphis=64)
+    fan_d = rt.get_ray_fan([0.5, -0.25, 1.0], 0.3, 101, 0.635, nphis=64, device=DEV).cpu().numpy()
+    assert fan_d.shape == fan_h.shape
+    assert np.allclose(fan_d, fan_h, rtol=0, atol=2e-15)
+
+
+def test_errors_are_loud():
+    system, m0, m1, rays, _ = build_case("c1_plano_convex")
+    with pytest.raises(ValueError):
+        system.ray_trace(rays, m0, m1, planes=[99])
+    with pytest.raises(ValueError):
+        rt.System(system.surfaces, system.materials).ray_trace(rays, m0, m1, planes="bogus")
+    with pytest.raises(C.RtpbError):
+        system.ray_trace(rays, m0, m1, devices=[1000])
+
+
+def test_empty_bundle():
+    system, m0, m1, rays, _ = build_case("c1_plano_convex")
+    out = system.ray_trace(rays[:0], m0, m1)
+    assert out.shape == (7, 0, 8)
+    out = system.ray_trace(torch.zeros((0, 8), dtype=torch.float64, device=DEV), m0, m1)
+    assert tuple(out.shape) == (7, 0, 8)
+
+
+def test_timing_counters():
+    system, m0, m1, rays, _ = build_case("c2_achromat")
+    lib = C.lib()
+    lib.rtpb_timing_enable(1)
+    x = torch.from_numpy(rays).to(DEV)
+    for _ in range(3):
+        system.ray_trace(x, m0, m1)
+    tot, cnt = ctypes.c_double(), ctypes.c_int64()
+    C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
+    lib.rtpb_timing_enable(0)
+    assert cnt.value == 3 and tot.value > 0
