@@ -105,7 +105,9 @@ int rtpb_shutdown(void);
 
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
 /* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,
-   System.materials, final material).  `dtype` is RTPB_F64 or RTPB_F32 (compute and storage type). */
+   System.materials, final material).  `dtype` is the STORAGE type of the ray buffers, RTPB_F64 or
+   RTPB_F32; arithmetic is always float64 (the reference's numerics), so an RTPB_F32 trace returns the
+   float64 result for the float32-rounded input, rounded once to float32 on store. */
 int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf,
                      const rtpb_material* materials, int32_t nmat,
                      int32_t dtype, rtpb_plan** plan_out);

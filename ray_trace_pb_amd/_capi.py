@@ -74,6 +74,14 @@ def lib():
                 raise RuntimeError(f"{LIB_PATH} not found: the HIP extension is not built. "
                                    "Run `python -c 'import __graft_entry__ as g; g.build()'` or "
                                    "`python -m ray_trace_pb_amd._build`.")
+            # One HIP runtime per process: PyTorch ships its own libamdhip64.so (same SONAME,
+            # libamdhip64.so.7, as /opt/rocm's).  If librtpb.so were loaded first it would pull in
+            # /opt/rocm's runtime and torch's copy, loaded later, would see no GPU.  Importing torch
+            # first makes librtpb.so bind to the runtime torch already mapped.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             handle = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(handle, name)

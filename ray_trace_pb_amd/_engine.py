@@ -18,11 +18,9 @@ import numpy as np
 
 from . import _capi as C
 
-# on-surface tolerance of the reference (RT:1343, 1408, 1528, 1597)
-ON_TOL_F64 = 1e-12
-# float32: the reference's absolute 1e-12 is below f32 resolution for any real geometry; use a
-# tolerance relative to the surface's own length scale (documented in DESIGN.md, "fp32 semantics")
-ON_TOL_F32_REL = 2.0 ** -12
+# on-surface tolerance of the reference (RT:1343, 1408, 1528, 1597).  The kernel computes in float64
+# for both storage types, so the reference's absolute tolerance applies unchanged.
+ON_TOL = 1e-12
 
 
 class Lowered:
@@ -34,16 +32,6 @@ def _f3(v):
     if a.size != 3:
         raise ValueError(f"expected a 3-vector, got {v!r}")
     return a
-
-
-def _surface_scale(s):
-    vals = [abs(float(x)) for x in np.asarray(s.center, dtype=float).ravel()]
-    vals.append(abs(float(getattr(s, "radius", 0.0) or 0.0)))
-    ap = float(s.aperture_rad)
-    if np.isfinite(ap):
-        vals.append(abs(ap))
-    vals.append(abs(float(getattr(s, "focal_len", 0.0) or 0.0)))
-    return max([1.0] + [v for v in vals if np.isfinite(v)])
 
 
 def lower(surfaces, materials, wavelengths, dtype):
@@ -67,7 +55,7 @@ def lower(surfaces, materials, wavelengths, dtype):
         d.input_axis[:] = _f3(s.input_axis)
         d.normal[:] = _f3(getattr(s, "normal", s.input_axis))
         d.aperture = float(s.aperture_rad)
-        d.on_tol = ON_TOL_F64 if dtype == C.RTPB_F64 else ON_TOL_F32_REL * _surface_scale(s)
+        d.on_tol = ON_TOL
         if kind == C.RTPB_SPHERE:
             d.radius = float(s.radius)
             d.radius_sq = float(s.radius ** 2)          # RT:1499 evaluates self.radius**2 on the host

@@ -14,8 +14,13 @@
 //   * per-ray failures are NaN selects, never divergent early exits, so a wave stays converged.
 // The surface loop is wave-uniform (same system for every lane), so its `kind` switches never diverge.
 //
+// Precision: arithmetic is ALWAYS float64 in registers (the reference's numerics); the storage type TS
+// of the ray buffers is float64 or float32.  float32 storage halves the HBM bytes (the bound) while the
+// values stay the correctly rounded float64 results: a float32 trace equals the float64 reference on the
+// float32-rounded input, rounded once on store.
+//
 // Memory roofline: per ray the kernel moves 8w bytes in and 8w bytes per stored plane out
-// (w = sizeof(T)); see DESIGN.md for the algorithmic-byte accounting used by bench.py.
+// (w = sizeof(TS)); see DESIGN.md for the algorithmic-byte accounting used by bench.py.
 
 #include <hip/hip_runtime.h>
 
@@ -65,13 +70,13 @@ struct DeviceGuard {
 };
 
 // ---------------------------------------------------------------------------------- kernel args
-template <typename T>
+template <typename TS>
 struct TraceArgs {
-    const T* __restrict__ in;
-    T* __restrict__ out;
-    const DevSurface<T>* __restrict__ surf;
-    const DevMaterial<T>* __restrict__ mats;
-    const T* __restrict__ table;
+    const TS* __restrict__ in;
+    TS* __restrict__ out;
+    const DevSurface<double>* __restrict__ surf;
+    const DevMaterial<double>* __restrict__ mats;
+    const double* __restrict__ table;
     int64_t n;
     int64_t in_fs;        // SOA input field stride
     int64_t out_ps;       // output plane (slot) stride
@@ -110,15 +115,11 @@ __device__ __forceinline__ DevMaterial<T> load_material(cptr<DevMaterial<T>> p) 
     return d;
 }
 
-template <typename T> struct Vec2;
-template <> struct Vec2<double> { using type = double2; };
-template <> struct Vec2<float> { using type = float2; };
-
-template <typename T, int LAYOUT>
-__device__ __forceinline__ Ray<T> load_ray(const T* __restrict__ in, int64_t i, int64_t fs) {
-    Ray<T> r;
+template <typename TS, int LAYOUT>
+__device__ __forceinline__ Ray<double> load_ray(const TS* __restrict__ in, int64_t i, int64_t fs) {
+    Ray<double> r;
     if constexpr (LAYOUT == RTPB_AOS) {
-        if constexpr (sizeof(T) == 8) {
+        if constexpr (sizeof(TS) == 8) {
             const double2* p = reinterpret_cast<const double2*>(in + i * 8);
             const double2 a = p[0], b = p[1], c = p[2], d = p[3];
             r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
@@ -134,10 +135,10 @@ __device__ __forceinline__ Ray<T> load_ray(const T* __restrict__ in, int64_t i, 
     return r;
 }
 
-template <typename T, int LAYOUT>
-__device__ __forceinline__ void store_ray(T* __restrict__ out, int64_t i, int64_t fs, const Ray<T>& r) {
+template <typename TS, int LAYOUT>
+__device__ __forceinline__ void store_ray(TS* __restrict__ out, int64_t i, int64_t fs, const Ray<double>& r) {
     if constexpr (LAYOUT == RTPB_AOS) {
-        if constexpr (sizeof(T) == 8) {
+        if constexpr (sizeof(TS) == 8) {
             double2* p = reinterpret_cast<double2*>(out + i * 8);
             p[0] = make_double2(r.x, r.y);
             p[1] = make_double2(r.z, r.dx);
@@ -145,12 +146,12 @@ __device__ __forceinline__ void store_ray(T* __restrict__ out, int64_t i, int64_
             p[3] = make_double2(r.ph, r.wl);
         } else {
             float4* p = reinterpret_cast<float4*>(out + i * 8);
-            p[0] = make_float4(r.x, r.y, r.z, r.dx);
-            p[1] = make_float4(r.dy, r.dz, r.ph, r.wl);
+            p[0] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
+            p[1] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
         }
     } else {
-        out[i] = r.x; out[fs + i] = r.y; out[2 * fs + i] = r.z; out[3 * fs + i] = r.dx;
-        out[4 * fs + i] = r.dy; out[5 * fs + i] = r.dz; out[6 * fs + i] = r.ph; out[7 * fs + i] = r.wl;
+        out[i] = TS(r.x); out[fs + i] = TS(r.y); out[2 * fs + i] = TS(r.z); out[3 * fs + i] = TS(r.dx);
+        out[4 * fs + i] = TS(r.dy); out[5 * fs + i] = TS(r.dz); out[6 * fs + i] = TS(r.ph); out[7 * fs + i] = TS(r.wl);
     }
 }
 
@@ -158,17 +159,19 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
     return p < 64 ? ((lo >> p) & 1ull) : ((hi >> (p - 64)) & 1ull);
 }
 
-// The fused multi-surface trace: one lane = one ray through all surfaces.
-template <typename T, int IN_LAYOUT, int OUT_LAYOUT>
-__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<T> a) {
+// The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
+// TS storage).
+template <typename TS, int IN_LAYOUT, int OUT_LAYOUT>
+__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
+    using T = double;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (i >= a.n) return;
-    Ray<T> r = load_ray<T, IN_LAYOUT>(a.in, i, a.in_fs);
+    Ray<T> r = load_ray<TS, IN_LAYOUT>(a.in, i, a.in_fs);
     const T wl0 = r.wl;
-    T* __restrict__ out = a.out;
+    TS* __restrict__ out = a.out;
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
-        store_ray<T, OUT_LAYOUT>(out, i, a.out_fs, r);
+        store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
         slot_off += a.out_ps;
     }
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
@@ -181,11 +184,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<T> a) {
         propagate_surface<T>(load_surface<T>(surf + s), r, n_cur, n_next, at, after);
         const int p = 2 * s + 1;
         if (plane_bit(a.mask_lo, a.mask_hi, p)) {
-            store_ray<T, OUT_LAYOUT>(out + slot_off, i, a.out_fs, at);
+            store_ray<TS, OUT_LAYOUT>(out + slot_off, i, a.out_fs, at);
             slot_off += a.out_ps;
         }
         if (plane_bit(a.mask_lo, a.mask_hi, p + 1)) {
-            store_ray<T, OUT_LAYOUT>(out + slot_off, i, a.out_fs, after);
+            store_ray<TS, OUT_LAYOUT>(out + slot_off, i, a.out_fs, after);
             slot_off += a.out_ps;
         }
         r = after;
@@ -212,13 +215,13 @@ __global__ __launch_bounds__(kBlock) void ray_fan_kernel(FanArgs<T> a) {
     const double tt = (a.n_thetas > 1 && it == a.n_thetas - 1) ? a.stop : double(it) * a.step + a.start;
     const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.nphis);
     const double ct = cos(tt), st = sin(tt), cp = cos(pp), sp = sin(pp);
-    Ray<T> r;
-    r.x = T(a.pt[0]); r.y = T(a.pt[1]); r.z = T(a.pt[2]);
-    r.dx = T(a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st);
-    r.dy = T(a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st);
-    r.dz = T(a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st);
-    r.ph = T(0);
-    r.wl = T(a.wl);
+    Ray<double> r;
+    r.x = a.pt[0]; r.y = a.pt[1]; r.z = a.pt[2];
+    r.dx = a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st;
+    r.dy = a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st;
+    r.dz = a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st;
+    r.ph = 0.0;
+    r.wl = a.wl;
     store_ray<T, RTPB_AOS>(a.out, k, 0, r);
 }
 
@@ -291,9 +294,7 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p, size_t& off_mats, size
 int plan_device_blob(rtpb_plan* p, int dev, void** out) {
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->blob[dev]) {
-        std::vector<unsigned char> host = p->dtype == RTPB_F64
-                                              ? build_blob<double>(*p, p->off_mats, p->off_table)
-                                              : build_blob<float>(*p, p->off_mats, p->off_table);
+        std::vector<unsigned char> host = build_blob<double>(*p, p->off_mats, p->off_table);
         DeviceGuard g(dev);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, host.size()));
@@ -349,13 +350,13 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int6
     if (rc) return rc;
     if (n == 0) return RTPB_OK;
     auto run = [&](auto tag) -> hipError_t {
-        using T = decltype(tag);
-        TraceArgs<T> a{};
-        a.in = static_cast<const T*>(in);
-        a.out = static_cast<T*>(out);
-        a.surf = reinterpret_cast<const DevSurface<T>*>(blob);
-        a.mats = reinterpret_cast<const DevMaterial<T>*>(static_cast<char*>(blob) + plan->off_mats);
-        a.table = reinterpret_cast<const T*>(static_cast<char*>(blob) + plan->off_table);
+        using TS = decltype(tag);
+        TraceArgs<TS> a{};
+        a.in = static_cast<const TS*>(in);
+        a.out = static_cast<TS*>(out);
+        a.surf = reinterpret_cast<const DevSurface<double>*>(blob);
+        a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
+        a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
         a.n = n;
         a.in_fs = in_fs;
         a.out_ps = out_ps;
@@ -363,7 +364,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int6
         a.mask_lo = lo;
         a.mask_hi = hi;
         a.nsurf = plan->nsurf;
-        return launch_trace<T>(a, il, ol, st);
+        return launch_trace<TS>(a, il, ol, st);
     };
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing.on) {

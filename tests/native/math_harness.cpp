@@ -12,45 +12,50 @@
 
 using namespace rtpb;
 
-extern "C" int harness_trace_f64(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials,
-                                 const double* in, int64_t n, double* out) {
-    std::vector<DevSurface<double>> S(nsurf);
+// TS = storage type of the ray buffers; arithmetic is float64 like the kernel
+template <typename TS>
+static int harness_trace(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials, const TS* in,
+                         int64_t n, TS* out) {
+    using T = double;
+    std::vector<DevSurface<T>> S(nsurf);
     for (int k = 0; k < nsurf; ++k) {
         const rtpb_surface& s = surfaces[k];
-        DevSurface<double>& d = S[k];
+        DevSurface<T>& d = S[k];
         d.kind = s.kind;
         for (int j = 0; j < 3; ++j) { d.c[j] = s.center[j]; d.nrm[j] = s.normal[j]; d.ax[j] = s.input_axis[j]; }
-        d.R = s.radius; d.R2 = s.radius_sq; d.absR = std::fabs(s.radius); d.ap = s.aperture;
-        d.f = s.focal_len; d.sin_a = s.sin_alpha; d.tol = s.on_tol;
+        d.R = T(s.radius); d.R2 = T(s.radius_sq); d.absR = T(std::fabs(s.radius)); d.ap = T(s.aperture);
+        d.f = T(s.focal_len); d.sin_a = T(s.sin_alpha); d.tol = T(s.on_tol);
     }
-    std::vector<DevMaterial<double>> M(nsurf + 1);
-    std::vector<double> table;
+    std::vector<DevMaterial<T>> M(nsurf + 1);
+    std::vector<T> table;
     for (int k = 0; k <= nsurf; ++k) {
         const rtpb_material& m = materials[k];
-        DevMaterial<double>& d = M[k];
+        DevMaterial<T>& d = M[k];
         d.kind = m.kind;
         bool zero = m.kind == RTPB_SELLMEIER;
-        for (int j = 0; j < 6; ++j) { d.c[j] = m.c[j]; zero = zero && m.c[j] == 0.0; }
+        for (int j = 0; j < 6; ++j) { d.c[j] = T(m.c[j]); zero = zero && m.c[j] == 0.0; }
         if (zero) d.kind = VACUUM;
         d.table_off = static_cast<int32_t>(table.size() / 2);
         d.table_len = m.kind == RTPB_TABLE ? m.table_len : 0;
-        if (m.kind == RTPB_TABLE) table.insert(table.end(), m.table, m.table + 2 * m.table_len);
+        if (m.kind == RTPB_TABLE)
+            for (int j = 0; j < 2 * m.table_len; ++j) table.push_back(T(m.table[j]));
     }
     const int64_t P = 2 * nsurf + 1;
     for (int64_t i = 0; i < n; ++i) {
-        const double* a = in + 8 * i;
-        Ray<double> r{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]};
-        auto put = [&](int64_t p, const Ray<double>& q) {
-            double* o = out + (p * n + i) * 8;
-            o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.dx; o[4] = q.dy; o[5] = q.dz; o[6] = q.ph; o[7] = q.wl;
+        const TS* a = in + 8 * i;
+        Ray<T> r{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]};
+        auto put = [&](int64_t p, const Ray<T>& q) {
+            TS* o = out + (p * n + i) * 8;
+            o[0] = TS(q.x); o[1] = TS(q.y); o[2] = TS(q.z); o[3] = TS(q.dx); o[4] = TS(q.dy); o[5] = TS(q.dz);
+            o[6] = TS(q.ph); o[7] = TS(q.wl);
         };
         put(0, r);
-        const double wl0 = r.wl;
-        double n_cur = material_n<double>(M[0], wl0, table.data());
+        const T wl0 = r.wl;
+        T n_cur = material_n<T>(M[0], wl0, table.data());
         for (int s = 0; s < nsurf; ++s) {
-            const double n_next = material_n<double>(M[s + 1], wl0, table.data());
-            Ray<double> at, after;
-            propagate_surface<double>(S[s], r, n_cur, n_next, at, after);
+            const T n_next = material_n<T>(M[s + 1], wl0, table.data());
+            Ray<T> at, after;
+            propagate_surface<T>(S[s], r, n_cur, n_next, at, after);
             put(2 * s + 1, at);
             put(2 * s + 2, after);
             r = after;
@@ -59,4 +64,14 @@ extern "C" int harness_trace_f64(const rtpb_surface* surfaces, int32_t nsurf, co
     }
     (void)P;
     return 0;
+}
+
+extern "C" int harness_trace_f64(const rtpb_surface* s, int32_t ns, const rtpb_material* m, const double* in,
+                                 int64_t n, double* out) {
+    return harness_trace<double>(s, ns, m, in, n, out);
+}
+
+extern "C" int harness_trace_f32(const rtpb_surface* s, int32_t ns, const rtpb_material* m, const float* in,
+                                 int64_t n, float* out) {
+    return harness_trace<float>(s, ns, m, in, n, out);
 }

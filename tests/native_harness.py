@@ -27,12 +27,13 @@ def harness():
     return _lib
 
 
-def harness_trace(low, rays2d):
+def harness_trace(low, rays2d, dtype=np.float64):
     """Full history (2S+1, N, 8) of rays2d through a lowered system (ray_trace_pb_amd._engine.lower)."""
-    rays2d = np.ascontiguousarray(rays2d, dtype=np.float64)
+    rays2d = np.ascontiguousarray(rays2d, dtype=dtype)
     n = rays2d.shape[0]
-    out = np.empty((2 * low.nsurf + 1, n, 8))
-    rc = harness().harness_trace_f64(low.surfaces, ctypes.c_int32(low.nsurf), low.materials,
+    out = np.empty((2 * low.nsurf + 1, n, 8), dtype=dtype)
+    fn = harness().harness_trace_f64 if dtype == np.float64 else harness().harness_trace_f32
+    rc = fn(low.surfaces, ctypes.c_int32(low.nsurf), low.materials,
                                      rays2d.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(n),
                                      out.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0

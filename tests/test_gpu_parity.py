@@ -135,12 +135,28 @@ def test_user_material_subclass_lowers_to_table():
     assert np.array_equal(got, ref, equal_nan=True)
 
 
-@pytest.mark.parametrize("name", ["c1_plano_convex", "c2_achromat", "c3_relay", "c4_opm", "c5_odt",
-                                  "kat_perfect_lens_phase", "reversed_doublet"])
+@pytest.mark.parametrize("name", CASES)
+def test_float32_storage_bitwise_vs_oracle_on_rounded_input(name):
+    """float32 mode = float32 storage, float64 arithmetic: the result is the float64 reference trace of
+    the float32-rounded input, rounded once to float32 -- bit for bit."""
+    system, m0, m1, rays, ref = build_case(name)
+    r32 = rays.astype(np.float32)
+    got = system.ray_trace(r32, m0, m1, dtype="float32")
+    assert got.dtype == np.float32
+    exp = oracle(system, m0, m1, r32.astype(np.float64)).astype(np.float32)
+    assert np.array_equal(got, exp, equal_nan=True)
+    got_t = system.ray_trace(torch.from_numpy(r32).to(DEV), m0, m1, dtype="float32")
+    assert got_t.dtype == torch.float32 and np.array_equal(got_t.cpu().numpy(), exp, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["c1_plano_convex", "c2_achromat", "c3_relay", "c4_mirror",
+                                  "kat_perfect_lens_phase", "reversed_doublet", "tir_prism"])
 def test_float32_within_1e5_of_float64_reference(name):
+    """Against the float64 reference on the ORIGINAL input: rtol 1e-5, column-scaled.
+    (c4_opm / c5_odt / stress are excluded: there the reference's absolute 1e-12 on-surface test itself
+    flips for some rays when the input is rounded to float32 -- the test above covers them exactly.)"""
     system, m0, m1, rays, ref = build_case(name)
     got = system.ray_trace(rays.astype(np.float32), m0, m1, dtype="float32")
-    assert got.dtype == np.float32
     ok, rep = compare(got, ref, rtol=1e-5)
     assert ok, rep
 
