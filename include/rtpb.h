@@ -142,6 +142,11 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
                  int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength,
                  void* stream);
 
+/* ---- tuning knobs (benchmarks / A-B tests; process-wide) ------------------------------------ */
+/* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
+   store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride. */
+int rtpb_set_tuning(const char* key, int64_t value);
+
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */
 /* While enabled on the calling thread, every trace kernel this thread launches is bracketed by a pair
    of HIP events recorded on the kernel's own stream.  rtpb_timing_collect() waits for them and

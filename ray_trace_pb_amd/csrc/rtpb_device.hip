@@ -159,19 +159,82 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
     return p < 64 ? ((lo >> p) & 1ull) : ((hi >> (p - 64)) & 1ull);
 }
 
+// ---------------------------------------------------------------------------------- AOS plane stores
+// A ray record is 8*sizeof(TS) = 64 B (f64) or 32 B (f32).  Stored directly, lane l writes its record
+// with 16-byte stores at a 64/32-byte lane stride: every store instruction touches 4 KiB of address
+// space at 25/50 % density and the history write (11 of 12 bytes moved) runs at ~3.4 TB/s.  Staged,
+// each wave first drops its 64 records into a private LDS tile, then lane l stores 16-byte chunks
+// l, l+64, ... of the wave's contiguous 4/2 KiB block: every global store instruction writes 1 KiB
+// contiguous.  The tile is XOR-swizzled so the b128 writes and reads are bank-conflict free:
+//   f64: chunk p of ray L lives at slot 4L + (p ^ ((L >> 1) & 3));  f32: 2L + (p ^ ((L >> 2) & 1)).
+// Only the owning wave touches its tile and LDS executes one wave's DS operations in order, so no
+// workgroup barrier is needed -- just the lgkmcnt waits (asm, with a memory clobber so the compiler
+// cannot move the tile accesses across them).
+constexpr int kWaves = kBlock / 64;
+constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
+
+template <typename TS>
+__device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
+                                                       int64_t n, int lane, const Ray<double>& r) {
+    if constexpr (sizeof(TS) == 8) {
+        const int sw = (lane >> 1) & 3;
+        double2* t = reinterpret_cast<double2*>(tile);
+        t[4 * lane + (0 ^ sw)] = make_double2(r.x, r.y);
+        t[4 * lane + (1 ^ sw)] = make_double2(r.z, r.dx);
+        t[4 * lane + (2 ^ sw)] = make_double2(r.dy, r.dz);
+        t[4 * lane + (3 ^ sw)] = make_double2(r.ph, r.wl);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
+        double2* g = reinterpret_cast<double2*>(plane + ray0 * 8);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
+            const double2 v = t[4 * rr + (pp ^ ((rr >> 1) & 3))];
+            if (c < nchunks) g[c] = v;
+        }
+    } else {
+        const int sw = (lane >> 2) & 1;
+        float4* t = reinterpret_cast<float4*>(tile);
+        t[2 * lane + (0 ^ sw)] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
+        t[2 * lane + (1 ^ sw)] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
+        float4* g = reinterpret_cast<float4*>(plane + ray0 * 8);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
+            const float4 v = t[2 * rr + (pp ^ ((rr >> 2) & 1))];
+            if (c < nchunks) g[c] = v;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
-// TS storage).
-template <typename TS, int IN_LAYOUT, int OUT_LAYOUT>
+// TS storage).  STAGED selects the LDS-staged AOS stores (OUT_LAYOUT == AOS only).
+template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, bool STAGED>
 __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
     using T = double;
+    __shared__ uint4 tiles[kWaves][kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    Ray<T> r = load_ray<TS, IN_LAYOUT>(a.in, i, a.in_fs);
+    const int64_t ray0 = i - lane;                       // first ray of this wave
+    if (ray0 >= a.n) return;                             // wave-uniform exit
+    const bool valid = i < a.n;
+    Ray<T> r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
     const T wl0 = r.wl;
     TS* __restrict__ out = a.out;
+    uint4* tile = tiles[threadIdx.x >> 6];
+    auto put = [&](int64_t off, const Ray<T>& q) {
+        if constexpr (STAGED && OUT_LAYOUT == RTPB_AOS) {
+            store_plane_aos_staged<TS>(tile, out + off, ray0, a.n, lane, q);
+        } else {
+            if (valid) store_ray<TS, OUT_LAYOUT>(out + off, i, a.out_fs, q);
+        }
+    };
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
-        store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
+        put(slot_off, r);
         slot_off += a.out_ps;
     }
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
@@ -184,11 +247,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
         propagate_surface<T>(load_surface<T>(surf + s), r, n_cur, n_next, at, after);
         const int p = 2 * s + 1;
         if (plane_bit(a.mask_lo, a.mask_hi, p)) {
-            store_ray<TS, OUT_LAYOUT>(out + slot_off, i, a.out_fs, at);
+            put(slot_off, at);
             slot_off += a.out_ps;
         }
         if (plane_bit(a.mask_lo, a.mask_hi, p + 1)) {
-            store_ray<TS, OUT_LAYOUT>(out + slot_off, i, a.out_fs, after);
+            put(slot_off, after);
             slot_off += a.out_ps;
         }
         r = after;
@@ -328,19 +391,26 @@ struct TimingState {
 };
 thread_local TimingState g_timing;
 
-template <typename T, int IL, int OL>
+// tuning knobs (rtpb_set_tuning); process-wide
+std::atomic<int> g_aos_staging{1};
+
+template <typename T, int IL, int OL, bool ST>
 hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
     const int64_t blocks = (a.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
     return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, hipStream_t st) {
-    if (il == RTPB_AOS && ol == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_AOS>(a, st);
-    if (il == RTPB_AOS && ol == RTPB_SOA) return launch_one<T, RTPB_AOS, RTPB_SOA>(a, st);
-    if (il == RTPB_SOA && ol == RTPB_AOS) return launch_one<T, RTPB_SOA, RTPB_AOS>(a, st);
-    return launch_one<T, RTPB_SOA, RTPB_SOA>(a, st);
+    const bool staged = g_aos_staging.load() != 0;
+    if (ol == RTPB_AOS) {
+        if (il == RTPB_AOS)
+            return staged ? launch_one<T, RTPB_AOS, RTPB_AOS, true>(a, st) : launch_one<T, RTPB_AOS, RTPB_AOS, false>(a, st);
+        return staged ? launch_one<T, RTPB_SOA, RTPB_AOS, true>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, false>(a, st);
+    }
+    if (il == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_SOA, false>(a, st);
+    return launch_one<T, RTPB_SOA, RTPB_SOA, false>(a, st);
 }
 
 int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int64_t in_fs, void* out, int ol,
@@ -602,6 +672,15 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     else return fail(RTPB_E_INVALID, "bad dtype");
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
+}
+
+int rtpb_set_tuning(const char* key, int64_t value) {
+    if (!key) return fail(RTPB_E_INVALID, "key is NULL");
+    if (std::strcmp(key, "aos_staging") == 0) {
+        g_aos_staging.store(value != 0);
+        return RTPB_OK;
+    }
+    return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);
 }
 
 int rtpb_timing_enable(int32_t on) {

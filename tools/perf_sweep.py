@@ -46,21 +46,22 @@ def main():
             x = torch.from_numpy(rays_np).to(dev, dtype=tdt)
             for planes in ("all", "final"):
                 sel = E.resolve_planes(planes, S)
-                for layout in ("aos", "soa"):
-                    lc = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
+                for layout in ("aos", "aos-direct", "soa"):
+                    lc = C.RTPB_SOA if layout == "soa" else C.RTPB_AOS
                     shape = (len(sel), n, 8) if lc == C.RTPB_AOS else (len(sel), 8, n)
                     out = torch.empty(shape, dtype=tdt, device=dev)
                     w = 8 if dtype == "f64" else 4
                     nbytes = n * 8 * w * (1 + len(sel))
                     name = f"{cfg}/{dtype}/{planes}/{layout}"
-                    variants.append((name, low, x, sel, lc, out, nbytes, n * S))
+                    variants.append((name, low, x, sel, lc, out, nbytes, n * S, 0 if layout == "aos-direct" else 1))
     # stream peak: device-to-device copy of 768 MB
     src = torch.empty(96_000_000, dtype=torch.float64, device=dev)
     dst = torch.empty_like(src)
     times = {v[0]: [] for v in variants}
     times["copy_768MB"] = []
     for _ in range(args.rounds):
-        for name, low, x, sel, lc, out, nbytes, units in variants:
+        for name, low, x, sel, lc, out, nbytes, units, staged in variants:
+            C.check(lib.rtpb_set_tuning(b"aos_staging", staged))
             E.trace_device(low, x, sel, layout_out=lc, out=out)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
@@ -78,7 +79,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         times["copy_768MB"].append(e0.elapsed_time(e1) / args.reps)
-    for name, low, x, sel, lc, out, nbytes, units in variants:
+    C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
+    for name, low, x, sel, lc, out, nbytes, units, staged in variants:
         ms = float(np.median(times[name]))
         res[name] = {"ms": ms, "GBps": nbytes / ms / 1e6, "ray_surf_per_s": units / ms * 1e3}
     ms = float(np.median(times["copy_768MB"]))
