@@ -136,11 +136,14 @@ def main():
     from ray_trace_pb_amd import _capi as C
     from ray_trace_pb_amd import _engine as E
 
-    dev = torch.device("cuda", local)
+    # one GPU per rank; the modulo only matters when rehearsing several ranks on one GPU
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     if world > 1:
+        # Control plane only (barriers + one max-reduction of the step time): rays are independent, so
+        # the trace has no data-path exchange and needs no RCCL communicator.
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")
 
     system, rays_np, m0, m1 = build_workload(rt, mat, args.rays, rank)
     S = len(system.surfaces)
@@ -187,7 +190,7 @@ def main():
     kernel_ms = tot_ms.value / max(launches.value, 1)
 
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms_max = t.tolist()
     else:

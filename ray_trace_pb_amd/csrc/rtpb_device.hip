@@ -33,7 +33,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/rtpb.h"
+#include "rtpb.h"
 #include "rtpb_math.h"
 
 using namespace rtpb;
@@ -173,7 +173,19 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
 constexpr int kWaves = kBlock / 64;
 constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 
-template <typename TS>
+typedef double v2d __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void gstore(double2* p, const double2& v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void gstore(float4* p, const float4& v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
+    else *p = v;
+}
+
+template <typename TS, bool NT>
 __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
                                                        int64_t n, int lane, const Ray<double>& r) {
     if constexpr (sizeof(TS) == 8) {
@@ -190,7 +202,7 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
         for (int j = 0; j < 4; ++j) {
             const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
             const double2 v = t[4 * rr + (pp ^ ((rr >> 1) & 3))];
-            if (c < nchunks) g[c] = v;
+            if (c < nchunks) gstore(g + c, v, NT);
         }
     } else {
         const int sw = (lane >> 2) & 1;
@@ -204,15 +216,16 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
         for (int j = 0; j < 2; ++j) {
             const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
             const float4 v = t[2 * rr + (pp ^ ((rr >> 2) & 1))];
-            if (c < nchunks) g[c] = v;
+            if (c < nchunks) gstore(g + c, v, NT);
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
-// TS storage).  STAGED selects the LDS-staged AOS stores (OUT_LAYOUT == AOS only).
-template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, bool STAGED>
+// TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
+// global stores for the staged tiles.
+template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE>
 __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
     using T = double;
     __shared__ uint4 tiles[kWaves][kTileBytes / 16];
@@ -226,8 +239,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
     TS* __restrict__ out = a.out;
     uint4* tile = tiles[threadIdx.x >> 6];
     auto put = [&](int64_t off, const Ray<T>& q) {
-        if constexpr (STAGED && OUT_LAYOUT == RTPB_AOS) {
-            store_plane_aos_staged<TS>(tile, out + off, ray0, a.n, lane, q);
+        if constexpr ((STORE & 1) && OUT_LAYOUT == RTPB_AOS) {
+            store_plane_aos_staged<TS, (STORE & 2) != 0>(tile, out + off, ray0, a.n, lane, q);
         } else {
             if (valid) store_ray<TS, OUT_LAYOUT>(out + off, i, a.out_fs, q);
         }
@@ -393,8 +406,9 @@ thread_local TimingState g_timing;
 
 // tuning knobs (rtpb_set_tuning); process-wide
 std::atomic<int> g_aos_staging{1};
+std::atomic<int> g_nt_stores{1};
 
-template <typename T, int IL, int OL, bool ST>
+template <typename T, int IL, int OL, int ST>
 hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
     const int64_t blocks = (a.n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
@@ -404,13 +418,16 @@ hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
 template <typename T>
 hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, hipStream_t st) {
     const bool staged = g_aos_staging.load() != 0;
+    const bool nt = g_nt_stores.load() != 0;
     if (ol == RTPB_AOS) {
-        if (il == RTPB_AOS)
-            return staged ? launch_one<T, RTPB_AOS, RTPB_AOS, true>(a, st) : launch_one<T, RTPB_AOS, RTPB_AOS, false>(a, st);
-        return staged ? launch_one<T, RTPB_SOA, RTPB_AOS, true>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, false>(a, st);
+        if (!staged)
+            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 0>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 0>(a, st);
+        if (nt)
+            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 3>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 3>(a, st);
+        return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 1>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 1>(a, st);
     }
-    if (il == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_SOA, false>(a, st);
-    return launch_one<T, RTPB_SOA, RTPB_SOA, false>(a, st);
+    if (il == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_SOA, 0>(a, st);
+    return launch_one<T, RTPB_SOA, RTPB_SOA, 0>(a, st);
 }
 
 int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int64_t in_fs, void* out, int ol,
@@ -678,6 +695,10 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     if (!key) return fail(RTPB_E_INVALID, "key is NULL");
     if (std::strcmp(key, "aos_staging") == 0) {
         g_aos_staging.store(value != 0);
+        return RTPB_OK;
+    }
+    if (std::strcmp(key, "nt_stores") == 0) {
+        g_nt_stores.store(value != 0);
         return RTPB_OK;
     }
     return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);

@@ -7,7 +7,7 @@
 #include <cstdint>
 #include <vector>
 
-#include "../../include/rtpb.h"
+#include "rtpb.h"
 #include "../../ray_trace_pb_amd/csrc/rtpb_math.h"
 
 using namespace rtpb;

@@ -18,11 +18,15 @@ _lib = None
 def harness():
     global _lib
     if _lib is None:
-        if not os.path.exists(OUT) or any(os.path.getmtime(OUT) < os.path.getmtime(d) for d in DEPS):
-            os.makedirs(os.path.dirname(OUT), exist_ok=True)
-            subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", OUT + ".tmp",
-                            SRC], check=True)
-            os.replace(OUT + ".tmp", OUT)
+        os.makedirs(os.path.dirname(OUT), exist_ok=True)
+        import fcntl
+        with open(OUT + ".lock", "w") as lk:        # several test processes may race to (re)build
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            if not os.path.exists(OUT) or any(os.path.getmtime(OUT) < os.path.getmtime(d) for d in DEPS):
+                tmp = f"{OUT}.{os.getpid()}.tmp"
+                subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+                                "-I", os.path.join(HERE, "..", "include"), "-o", tmp, SRC], check=True)
+                os.replace(tmp, OUT)
         _lib = ctypes.CDLL(OUT)
     return _lib
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--configs", default="c2")
+    ap.add_argument("--only", default="", help="comma list of variant-name substrings to keep")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = C.lib()
@@ -46,14 +47,18 @@ def main():
             x = torch.from_numpy(rays_np).to(dev, dtype=tdt)
             for planes in ("all", "final"):
                 sel = E.resolve_planes(planes, S)
-                for layout in ("aos", "aos-direct", "soa"):
+                for layout in ("aos", "aos-nt", "aos-direct", "soa"):
                     lc = C.RTPB_SOA if layout == "soa" else C.RTPB_AOS
                     shape = (len(sel), n, 8) if lc == C.RTPB_AOS else (len(sel), 8, n)
                     out = torch.empty(shape, dtype=tdt, device=dev)
                     w = 8 if dtype == "f64" else 4
                     nbytes = n * 8 * w * (1 + len(sel))
                     name = f"{cfg}/{dtype}/{planes}/{layout}"
-                    variants.append((name, low, x, sel, lc, out, nbytes, n * S, 0 if layout == "aos-direct" else 1))
+                    mode = {"aos": 1, "aos-nt": 3, "aos-direct": 0, "soa": 0}[layout]
+                    variants.append((name, low, x, sel, lc, out, nbytes, n * S, mode))
+    if args.only:
+        keep = args.only.split(",")
+        variants = [v for v in variants if any(k in v[0] for k in keep)]
     # stream peak: device-to-device copy of 768 MB
     src = torch.empty(96_000_000, dtype=torch.float64, device=dev)
     dst = torch.empty_like(src)
@@ -61,7 +66,8 @@ def main():
     times["copy_768MB"] = []
     for _ in range(args.rounds):
         for name, low, x, sel, lc, out, nbytes, units, staged in variants:
-            C.check(lib.rtpb_set_tuning(b"aos_staging", staged))
+            C.check(lib.rtpb_set_tuning(b"aos_staging", staged & 1))
+            C.check(lib.rtpb_set_tuning(b"nt_stores", staged >> 1))
             E.trace_device(low, x, sel, layout_out=lc, out=out)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
@@ -80,6 +86,7 @@ def main():
         torch.cuda.synchronize()
         times["copy_768MB"].append(e0.elapsed_time(e1) / args.reps)
     C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
+    C.check(lib.rtpb_set_tuning(b"nt_stores", 1))
     for name, low, x, sel, lc, out, nbytes, units, staged in variants:
         ms = float(np.median(times[name]))
         res[name] = {"ms": ms, "GBps": nbytes / ms / 1e6, "ray_surf_per_s": units / ms * 1e3}
