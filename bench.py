@@ -42,8 +42,8 @@ def shard_seed(rank):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU")
     ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
     ap.add_argument("--planes", default="all", choices=["all", "final"])

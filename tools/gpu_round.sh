@@ -19,9 +19,9 @@ step() {  # name timeout cmd...
 }
 step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:warnings
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps 50 --warmup 5
+step bench 600 python bench.py
 step bench_2ranks_1gpu 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 3
-step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof -o bench -- python3 bench.py --steps 20 --warmup 3 --cpu-baseline off --traffic off
+step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof -o bench -- python3 bench.py --cpu-baseline off --traffic off
 step pmc_all 900 bash tools/pmc_profile.sh $P/pmc_all --planes all
 step pmc_final 900 bash tools/pmc_profile.sh $P/pmc_final --planes final
 step sweep 600 python tools/perf_sweep.py --configs c2,c5,c4
