@@ -146,7 +146,9 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
 /* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.
    "nt_stores": 1 (default) = non-temporal global stores for the staged AOS tiles (the history is
-   streamed out and never re-read by the kernel); 0 = default cache policy. */
+   streamed out and never re-read by the kernel); 0 = default cache policy.
+   "waves_per_eu": 0 (default: compiler choice, 4 waves/SIMD) or 5 / 6 = occupancy target for the
+   AOS->AOS staged kernel (the compiler then spills to scratch to fit). */
 int rtpb_set_tuning(const char* key, int64_t value);
 
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */

@@ -141,13 +141,32 @@ def _np_dtype(dtype):
     return np.float64 if dtype == C.RTPB_F64 else np.float32
 
 
+PINNED_MIN_BYTES = 32 << 20
+
+
+def host_empty(shape, dtype):
+    """Output array for the NumPy path.  Large outputs come from PyTorch's pinned (page-locked)
+    caching host allocator: the GPU DMAs straight into them, and a freed array's pages go back to
+    the cache already faulted in -- a fresh np.empty of the C2 history (704 MB) costs ~60 ms of
+    first-touch page faults, more than the whole trace.  The result is an ordinary ndarray."""
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    if nbytes >= PINNED_MIN_BYTES:
+        try:
+            import torch
+            tdt = torch.float64 if np.dtype(dtype) == np.float64 else torch.float32
+            return torch.empty(tuple(shape), dtype=tdt, pin_memory=True).numpy()
+        except Exception:       # no torch / no pinned memory: fall back to pageable memory
+            pass
+    return np.empty(shape, dtype=dtype)
+
+
 def trace_host(low, rays2d, planes, devices=None, out=None):
     """NumPy (N, 8) -> NumPy (len(planes), N, 8)."""
     plan = plan_for(low)
     rays2d = np.ascontiguousarray(rays2d, dtype=_np_dtype(low.dtype))
     n = rays2d.shape[0]
     if out is None:
-        out = np.empty((len(planes), n, 8), dtype=rays2d.dtype)
+        out = host_empty((len(planes), n, 8), rays2d.dtype)
     lo, hi = plane_mask(planes)
     if devices is None:
         devs = None

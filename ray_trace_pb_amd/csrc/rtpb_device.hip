@@ -225,8 +225,8 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
 // TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
 // global stores for the staged tiles.
-template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE>
-__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs<TS> a) {
+template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void trace_kernel(TraceArgs<TS> a) {
     using T = double;
     __shared__ uint4 tiles[kWaves][kTileBytes / 16];
     const int lane = threadIdx.x & 63;
@@ -407,12 +407,23 @@ thread_local TimingState g_timing;
 // tuning knobs (rtpb_set_tuning); process-wide
 std::atomic<int> g_aos_staging{1};
 std::atomic<int> g_nt_stores{1};
+std::atomic<int> g_waves_per_eu{0};
+
+template <typename T, int IL, int OL, int ST, int W>
+hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
+    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
 
 template <typename T, int IL, int OL, int ST>
 hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
-    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
-    return hipGetLastError();
+    if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
+        const int w = g_waves_per_eu.load();
+        if (w == 5) return launch_w<T, IL, OL, ST, 5>(a, st);
+        if (w == 6) return launch_w<T, IL, OL, ST, 6>(a, st);
+    }
+    return launch_w<T, IL, OL, ST, 1>(a, st);
 }
 
 template <typename T>
@@ -473,6 +484,121 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int6
     return RTPB_OK;
 }
 
+// ---------------------------------------------------------------------------------- host pipeline
+// NumPy-in / NumPy-out path.  Pageable host memory caps PCIe copies at ~11 GB/s, so each device keeps a
+// cached set of pinned staging buffers and runs a two-deep pipeline over ray chunks:
+//   CPU: input chunk k -> pinned_in[k%2];  GPU stream: H2D(k) -> trace(k) -> D2H(k) into pinned_out[k%2]
+//   CPU (overlapping GPU chunk k): scatter pinned_out[(k-1)%2] into every output plane, multi-threaded.
+struct HostStage {
+    std::mutex mu;                 // one rtpb_trace_host call per device at a time
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    void* pin_in[2] = {nullptr, nullptr};
+    void* pin_out[2] = {nullptr, nullptr};
+    void* d_in[2] = {nullptr, nullptr};
+    void* d_out[2] = {nullptr, nullptr};
+    size_t in_bytes = 0, out_bytes = 0;
+};
+HostStage g_stage[kMaxDevices];
+
+int stage_reserve(HostStage& hs, size_t in_bytes, size_t out_bytes) {
+    if (!hs.st) {
+        HIP_TRY(hipStreamCreateWithFlags(&hs.st, hipStreamNonBlocking));
+        for (auto& e : hs.ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (in_bytes > hs.in_bytes || out_bytes > hs.out_bytes) {
+        for (int k = 0; k < 2; ++k) {
+            if (hs.pin_in[k]) (void)hipHostFree(hs.pin_in[k]);
+            if (hs.pin_out[k]) (void)hipHostFree(hs.pin_out[k]);
+            if (hs.d_in[k]) (void)hipFree(hs.d_in[k]);
+            if (hs.d_out[k]) (void)hipFree(hs.d_out[k]);
+            hs.pin_in[k] = hs.pin_out[k] = hs.d_in[k] = hs.d_out[k] = nullptr;
+        }
+        hs.in_bytes = hs.out_bytes = 0;
+        for (int k = 0; k < 2; ++k) {
+            HIP_TRY(hipHostMalloc(&hs.pin_in[k], in_bytes, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&hs.pin_out[k], out_bytes, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&hs.d_in[k], in_bytes));
+            HIP_TRY(hipMalloc(&hs.d_out[k], out_bytes));
+        }
+        hs.in_bytes = in_bytes;
+        hs.out_bytes = out_bytes;
+    }
+    return RTPB_OK;
+}
+
+// parallel memcpy of `count` equally sized pieces (piece i: dst_i <- src_i) over T threads
+void parallel_scatter(char* out, const char* staged, int nslots, int64_t slot_stride_bytes, int64_t piece_bytes,
+                      int T) {
+    const int64_t total = piece_bytes * nslots;
+    const int64_t per = (total + T - 1) / T;
+    auto job = [&](int t) {
+        int64_t lo = t * per, hi = std::min<int64_t>(total, lo + per);
+        while (lo < hi) {
+            const int64_t s = lo / piece_bytes, off = lo % piece_bytes;
+            const int64_t len = std::min<int64_t>(hi - lo, piece_bytes - off);
+            std::memcpy(out + s * slot_stride_bytes + off, staged + s * piece_bytes + off, static_cast<size_t>(len));
+            lo += len;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(job, t);
+    job(0);
+    for (auto& x : th) x.join();
+}
+
+bool is_pinned_host(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+int host_shard_pipeline(rtpb_plan* plan, int dev, const char* in, char* out, int64_t n_rays, int64_t a, int64_t b,
+                        size_t rec, int nslots, uint64_t lo, uint64_t hi, int T) {
+    HostStage& hs = g_stage[dev];
+    std::lock_guard<std::mutex> lk(hs.mu);
+    DeviceGuard guard(dev);
+    // pinned (page-locked, e.g. torch pin_memory) output: DMA every plane slice straight into place
+    const bool direct = is_pinned_host(out) && is_pinned_host(out + (int64_t(nslots) * n_rays * rec - 1));
+    // ~128 MiB of output per chunk (at least 64k rays), two chunks in flight
+    const int64_t chunk = std::min<int64_t>(b - a, std::max<int64_t>(1 << 16, (int64_t(128) << 20) / int64_t(nslots * rec)));
+    int rc = stage_reserve(hs, chunk * rec, chunk * rec * nslots);
+    if (rc) return rc;
+    const int64_t nchunks = (b - a + chunk - 1) / chunk;
+    auto scatter = [&](int64_t k) -> int {
+        const int buf = static_cast<int>(k & 1);
+        HIP_TRY(hipEventSynchronize(hs.ev[buf]));
+        if (direct) return RTPB_OK;
+        const int64_t c0 = a + k * chunk, m = std::min<int64_t>(chunk, b - c0);
+        parallel_scatter(out + c0 * rec, static_cast<const char*>(hs.pin_out[buf]), nslots,
+                         static_cast<int64_t>(n_rays * rec), static_cast<int64_t>(m * rec), T);
+        return RTPB_OK;
+    };
+    for (int64_t k = 0; k < nchunks; ++k) {
+        const int buf = static_cast<int>(k & 1);
+        const int64_t c0 = a + k * chunk, m = std::min<int64_t>(chunk, b - c0);
+        // pin_in[buf] / pin_out[buf] were last used by chunk k-2, whose event was waited in scatter(k-2)
+        std::memcpy(hs.pin_in[buf], in + c0 * rec, static_cast<size_t>(m * rec));
+        HIP_TRY(hipMemcpyAsync(hs.d_in[buf], hs.pin_in[buf], m * rec, hipMemcpyHostToDevice, hs.st));
+        rc = trace_impl(plan, dev, hs.d_in[buf], m, RTPB_AOS, 0, hs.d_out[buf], RTPB_AOS, m * 8, 0, lo, hi, hs.st);
+        if (rc) return rc;
+        if (direct)
+            HIP_TRY(hipMemcpy2DAsync(out + c0 * rec, n_rays * rec, hs.d_out[buf], m * rec, m * rec, nslots,
+                                     hipMemcpyDeviceToHost, hs.st));
+        else
+            HIP_TRY(hipMemcpyAsync(hs.pin_out[buf], hs.d_out[buf], m * rec * nslots, hipMemcpyDeviceToHost, hs.st));
+        HIP_TRY(hipEventRecord(hs.ev[buf], hs.st));
+        if (k >= 1) {
+            rc = scatter(k - 1);
+            if (rc) return rc;
+        }
+    }
+    return scatter(nchunks - 1);
+}
+
 }  // namespace
 
 // ================================================================================== C ABI
@@ -488,7 +614,28 @@ int rtpb_device_count(void) {
     return n;
 }
 
-int rtpb_shutdown(void) { return RTPB_OK; }
+int rtpb_shutdown(void) {
+    for (int d = 0; d < kMaxDevices; ++d) {
+        HostStage& hs = g_stage[d];
+        std::lock_guard<std::mutex> lk(hs.mu);
+        if (!hs.st) continue;
+        DeviceGuard g(d);
+        (void)hipStreamSynchronize(hs.st);
+        for (int k = 0; k < 2; ++k) {
+            if (hs.pin_in[k]) (void)hipHostFree(hs.pin_in[k]);
+            if (hs.pin_out[k]) (void)hipHostFree(hs.pin_out[k]);
+            if (hs.d_in[k]) (void)hipFree(hs.d_in[k]);
+            if (hs.d_out[k]) (void)hipFree(hs.d_out[k]);
+            hs.pin_in[k] = hs.pin_out[k] = hs.d_in[k] = hs.d_out[k] = nullptr;
+            (void)hipEventDestroy(hs.ev[k]);
+            hs.ev[k] = nullptr;
+        }
+        (void)hipStreamDestroy(hs.st);
+        hs.st = nullptr;
+        hs.in_bytes = hs.out_bytes = 0;
+    }
+    return RTPB_OK;
+}
 
 int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials, int32_t nmat,
                      int32_t dtype, rtpb_plan** plan_out) {
@@ -596,49 +743,17 @@ int rtpb_trace_host(const rtpb_plan* plan_c, const void* rays_in, int64_t n_rays
     const size_t w = plan->dtype == RTPB_F64 ? 8 : 4;
     const size_t rec = 8 * w;
     const int G = static_cast<int>(devs.size());
+    // host threads that scatter staged chunks into the caller's array, per device
+    const unsigned hw = std::max(2u, std::thread::hardware_concurrency());
+    const int copy_threads = static_cast<int>(std::max(2u, std::min(16u, hw / static_cast<unsigned>(G))));
     std::vector<int> rcs(G, RTPB_OK);
     std::vector<std::string> errs(G);
     auto worker = [&](int g) {
         const int dev = devs[g];
         const int64_t a = n_rays * g / G, b = n_rays * (g + 1) / G;
         if (b <= a) return;
-        auto body = [&]() -> int {
-            DeviceGuard guard(dev);
-            // chunk so that one chunk's output stays <= ~1 GiB of device memory
-            const int64_t max_chunk = std::max<int64_t>(1 << 16, (int64_t(1) << 30) / int64_t(nslots * rec));
-            const int64_t chunk = std::min<int64_t>(b - a, max_chunk);
-            hipStream_t st = nullptr;
-            HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-            void *d_in = nullptr, *d_out = nullptr;
-            int rc = RTPB_OK;
-            auto cleanup = [&]() {
-                if (d_in) (void)hipFree(d_in);
-                if (d_out) (void)hipFree(d_out);
-                (void)hipStreamDestroy(st);
-            };
-            hipError_t e = hipMalloc(&d_in, chunk * rec);
-            if (e == hipSuccess) e = hipMalloc(&d_out, chunk * rec * nslots);
-            if (e != hipSuccess) {
-                cleanup();
-                return fail(RTPB_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
-            }
-            for (int64_t c0 = a; c0 < b && rc == RTPB_OK; c0 += chunk) {
-                const int64_t m = std::min<int64_t>(chunk, b - c0);
-                e = hipMemcpyAsync(d_in, static_cast<const char*>(rays_in) + c0 * rec, m * rec,
-                                   hipMemcpyHostToDevice, st);
-                if (e != hipSuccess) { rc = fail(RTPB_E_HIP, std::string("H2D: ") + hipGetErrorString(e)); break; }
-                rc = trace_impl(plan, dev, d_in, m, RTPB_AOS, 0, d_out, RTPB_AOS, m * 8, 0, plane_mask_lo,
-                                plane_mask_hi, st);
-                if (rc) break;
-                e = hipMemcpy2DAsync(static_cast<char*>(out) + c0 * rec, n_rays * rec, d_out, m * rec, m * rec,
-                                     nslots, hipMemcpyDeviceToHost, st);
-                if (e == hipSuccess) e = hipStreamSynchronize(st);
-                if (e != hipSuccess) rc = fail(RTPB_E_HIP, std::string("D2H: ") + hipGetErrorString(e));
-            }
-            cleanup();
-            return rc;
-        };
-        rcs[g] = body();
+        rcs[g] = host_shard_pipeline(plan, dev, static_cast<const char*>(rays_in), static_cast<char*>(out), n_rays, a,
+                                     b, rec, nslots, plane_mask_lo, plane_mask_hi, copy_threads);
         if (rcs[g]) errs[g] = g_last_error;
     };
     if (G == 1) {
@@ -699,6 +814,11 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     }
     if (std::strcmp(key, "nt_stores") == 0) {
         g_nt_stores.store(value != 0);
+        return RTPB_OK;
+    }
+    if (std::strcmp(key, "waves_per_eu") == 0) {
+        if (value != 0 && value != 5 && value != 6) return fail(RTPB_E_INVALID, "waves_per_eu must be 0, 5 or 6");
+        g_waves_per_eu.store(static_cast<int>(value));
         return RTPB_OK;
     }
     return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);

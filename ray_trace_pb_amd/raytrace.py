@@ -266,7 +266,7 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
         raise ValueError("layout='soa' is only available for device (torch CUDA) inputs")
     devs = _resolve_devices(devices)
     if full and k > 1:
-        out = np.empty((k - 1 + len(sel), n, 8), dtype=np.float64 if code == C.RTPB_F64 else np.float32)
+        out = E.host_empty((k - 1 + len(sel), n, 8), np.float64 if code == C.RTPB_F64 else np.float32)
         out[:k] = rays
         E.trace_host(low, last, sel[1:], devs, out=out[k:])
         return out

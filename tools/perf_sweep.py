@@ -47,14 +47,15 @@ def main():
             x = torch.from_numpy(rays_np).to(dev, dtype=tdt)
             for planes in ("all", "final"):
                 sel = E.resolve_planes(planes, S)
-                for layout in ("aos", "aos-nt", "aos-direct", "soa"):
+                for layout in ("aos", "aos-nt", "aos-nt-w5", "aos-nt-w6", "aos-direct", "soa"):
                     lc = C.RTPB_SOA if layout == "soa" else C.RTPB_AOS
                     shape = (len(sel), n, 8) if lc == C.RTPB_AOS else (len(sel), 8, n)
                     out = torch.empty(shape, dtype=tdt, device=dev)
                     w = 8 if dtype == "f64" else 4
                     nbytes = n * 8 * w * (1 + len(sel))
                     name = f"{cfg}/{dtype}/{planes}/{layout}"
-                    mode = {"aos": 1, "aos-nt": 3, "aos-direct": 0, "soa": 0}[layout]
+                    mode = {"aos": 1, "aos-nt": 3, "aos-nt-w5": 3 + 5 * 4, "aos-nt-w6": 3 + 6 * 4, "aos-direct": 0,
+                            "soa": 0}[layout]
                     variants.append((name, low, x, sel, lc, out, nbytes, n * S, mode))
     if args.only:
         keep = args.only.split(",")
@@ -67,7 +68,8 @@ def main():
     for _ in range(args.rounds):
         for name, low, x, sel, lc, out, nbytes, units, staged in variants:
             C.check(lib.rtpb_set_tuning(b"aos_staging", staged & 1))
-            C.check(lib.rtpb_set_tuning(b"nt_stores", staged >> 1))
+            C.check(lib.rtpb_set_tuning(b"nt_stores", (staged >> 1) & 1))
+            C.check(lib.rtpb_set_tuning(b"waves_per_eu", staged >> 2))
             E.trace_device(low, x, sel, layout_out=lc, out=out)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
@@ -87,6 +89,7 @@ def main():
         times["copy_768MB"].append(e0.elapsed_time(e1) / args.reps)
     C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
     C.check(lib.rtpb_set_tuning(b"nt_stores", 1))
+    C.check(lib.rtpb_set_tuning(b"waves_per_eu", 0))
     for name, low, x, sel, lc, out, nbytes, units, staged in variants:
         ms = float(np.median(times[name]))
         res[name] = {"ms": ms, "GBps": nbytes / ms / 1e6, "ray_surf_per_s": units / ms * 1e3}
