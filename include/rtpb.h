@@ -142,6 +142,25 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
                  int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength,
                  void* stream);
 
+/* get_collimated_rays(pt, displacement_max, n_disps, wavelength, nphis, phi_start, normal) (RT:99-161):
+   ray k = idisp*nphis + iphi; `normal` must be a unit vector. */
+int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
+                         int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
+                         void* stream);
+
+/* ---- device analysis ------------------------------------------------------------------------- */
+/* intersect_rays(ray1, ray2) (RT:164-238) on device rays (AOS, n x 8; a length-1 side broadcasts).
+   pts_out: max(n1, n2) x 3 intersection points, NaN where the rays do not meet within 1e-12. */
+int rtpb_intersect_rays(int32_t device, int32_t dtype, const void* ray1, int64_t n1, const void* ray2, int64_t n2,
+                        void* pts_out, void* stream);
+/* Spot statistics of one (N, 8) AOS plane split into n_groups contiguous groups of group_size rays
+   (e.g. one group per (field point, wavelength) fan).  Rays with non-finite x or y are skipped.
+   stats_out (device, n_groups x 7 doubles): count, sum x, sum y, sum z, sum x^2, sum y^2, sum x*y.
+   Deterministic (fixed-order two-pass reduction).  workspace: device doubles,
+   >= n_groups * ceil(group_size / 256) * 7. */
+int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t group_size, int64_t n_groups,
+                    double* workspace, int64_t workspace_len, double* stats_out, void* stream);
+
 /* ---- tuning knobs (benchmarks / A-B tests; process-wide) ------------------------------------ */
 /* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.

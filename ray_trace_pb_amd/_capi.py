@@ -51,6 +51,10 @@ SIGNATURES = {
     "rtpb_trace_host": (ctypes.c_int, [_P, _P, _i64, _P, _u64, _u64, ctypes.POINTER(_i32), _i32]),
     "rtpb_ray_fan": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, ctypes.POINTER(_dbl),
                                     _dbl, _P]),
+    "rtpb_collimated_rays": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, _dbl,
+                                            ctypes.POINTER(_dbl), _dbl, _P]),
+    "rtpb_intersect_rays": (ctypes.c_int, [_i32, _i32, _P, _i64, _P, _i64, _P, _P]),
+    "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),
     "rtpb_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "rtpb_timing_enable": (ctypes.c_int, [_i32]),
     "rtpb_timing_collect": (ctypes.c_int, [ctypes.POINTER(_dbl), ctypes.POINTER(_i64)]),

@@ -1,0 +1,101 @@
+"""Device-side analysis of traced bundles: spot statistics per (field, wavelength)
+group and a chunked spot-diagram sweep that never leaves HBM (BASELINE configs[4] / C5 scale).
+
+The reference computes spot diagrams in user scripts with NumPy on the full host history; here the
+fans are generated on the GPU (``rtpb_ray_fan``), traced with only the final plane stored, and reduced
+on the GPU with a deterministic fixed-order reduction (``rtpb_spot_stats``).
+"""
+import time
+
+import numpy as np
+
+from . import _capi as C
+from . import _engine as E
+
+STAT_NAMES = ("count", "sum_x", "sum_y", "sum_z", "sum_xx", "sum_yy", "sum_xy")
+
+
+def spot_stats_raw(plane, group_size, stream=None):
+    """Per-group sums (n_groups, 7) of a torch CUDA (N, 8) plane, N = n_groups * group_size."""
+    import torch
+    n = plane.shape[0]
+    if n % group_size:
+        raise ValueError("plane length must be a multiple of group_size")
+    ngroups = n // group_size
+    plane = plane.contiguous()
+    tiles = -(-group_size // 256)
+    ws = torch.empty(ngroups * tiles * 7, dtype=torch.float64, device=plane.device)
+    stats = torch.empty((ngroups, 7), dtype=torch.float64, device=plane.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(plane.device).cuda_stream
+    C.check(C.lib().rtpb_spot_stats(plane.device.index or 0,
+                                    C.RTPB_F64 if plane.dtype == torch.float64 else C.RTPB_F32,
+                                    plane.data_ptr(), group_size, ngroups, ws.data_ptr(), ws.numel(),
+                                    stats.data_ptr(), stream))
+    return stats
+
+
+def summarize(raw):
+    """count, centroid (x, y, z) and RMS spot radius about the centroid from the raw sums."""
+    raw = np.asarray(raw, dtype=np.float64)
+    n = raw[..., 0]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        cx, cy, cz = raw[..., 1] / n, raw[..., 2] / n, raw[..., 3] / n
+        var = raw[..., 4] / n - cx * cx + raw[..., 5] / n - cy * cy
+    return {"count": n, "centroid": np.stack((cx, cy, cz), axis=-1), "rms_radius": np.sqrt(np.maximum(var, 0.0))}
+
+
+def spot_stats(plane, group_size):
+    """Spot summary per contiguous group of ``group_size`` rays of a torch CUDA (N, 8) plane."""
+    return summarize(spot_stats_raw(plane, group_size).cpu().numpy())
+
+
+def spot_sweep(system, initial_material, final_material, field_points, wavelengths, theta_max, n_thetas, nphis=1,
+               center_ray=(0, 0, 1), device="cuda:0", dtype="float64", groups_per_batch=None):
+    """Spot diagrams for every (field point, wavelength): a ``get_ray_fan(field, theta_max, n_thetas,
+    wavelength, nphis)`` bundle per group, generated, traced (final plane only) and reduced on the GPU.
+
+    Returns (summary dict with arrays shaped (n_fields, n_wavelengths, ...), timing dict).  Groups are
+    processed in batches that reuse the same HBM buffers."""
+    import torch
+    dev = torch.device(device)
+    tdt = torch.float64 if dtype in ("float64", np.float64) else torch.float32
+    code = C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32
+    if np.linalg.norm(np.asarray(center_ray, dtype=float)) != 1:
+        raise ValueError("center_ray must be a unit vector")
+    field_points = np.atleast_2d(np.asarray(field_points, dtype=float))
+    wavelengths = np.atleast_1d(np.asarray(wavelengths, dtype=float))
+    G = field_points.shape[0] * wavelengths.size
+    per = n_thetas * nphis
+    if groups_per_batch is None:
+        groups_per_batch = max(1, min(G, (1 << 27) // per))     # ~128M rays in flight
+    mats = [initial_material] + list(system.materials) + [final_material]
+    low = E.lower(system.surfaces, mats, lambda: np.unique(wavelengths), code)
+    sel = E.resolve_planes("final", len(system.surfaces))
+    S = len(system.surfaces)
+    rays = torch.empty((groups_per_batch * per, 8), dtype=tdt, device=dev)
+    out = torch.empty((1, groups_per_batch * per, 8), dtype=tdt, device=dev)
+    raw = np.zeros((G, 7))
+    jobs = [(f, w) for f in range(field_points.shape[0]) for w in range(wavelengths.size)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for b0 in range(0, G, groups_per_batch):
+        batch = jobs[b0:b0 + groups_per_batch]
+        for k, (f, w) in enumerate(batch):       # generate each fan in place in the batch buffer
+            _fan_into(rays[k * per:(k + 1) * per], field_points[f], theta_max, n_thetas, wavelengths[w], nphis,
+                      center_ray, code)
+        m = len(batch) * per
+        E.trace_device(low, rays[:m], sel, out=out[:, :m])
+        raw[b0:b0 + len(batch)] = spot_stats_raw(out[0, :m], per).cpu().numpy()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    summ = summarize(raw.reshape(field_points.shape[0], wavelengths.size, 7))
+    return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt}
+
+
+def _fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray, code):
+    import torch
+    d3 = C.ctypes.c_double * 3
+    C.check(C.lib().rtpb_ray_fan(buf.device.index or 0, code, buf.data_ptr(), d3(*np.asarray(pt, dtype=float).ravel()),
+                                 float(theta_max), int(n_thetas), int(nphis), d3(*np.asarray(center_ray, dtype=float)),
+                                 float(wavelength), torch.cuda.current_stream(buf.device).cuda_stream))

@@ -301,6 +301,125 @@ __global__ __launch_bounds__(kBlock) void ray_fan_kernel(FanArgs<T> a) {
     store_ray<T, RTPB_AOS>(a.out, k, 0, r);
 }
 
+// get_collimated_rays (RT:99-161) on the device: ray k = idisp * nphis + iphi, position
+// pt + n1 * (off cos phi) + n2 * (off sin phi), direction = normal.
+struct CollArgs {
+    void* __restrict__ out;
+    int64_t n_disps, nphis;
+    double pt[3], n1[3], n2[3], nrm[3];
+    double start, stop, step, phi_start, wl;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void collimated_kernel(CollArgs a) {
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (k >= a.n_disps * a.nphis) return;
+    const int64_t id = k / a.nphis, ip = k % a.nphis;
+    const double oo = (a.n_disps > 1 && id == a.n_disps - 1) ? a.stop : double(id) * a.step + a.start;
+    const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.nphis) + a.phi_start;
+    const double oc = oo * cos(pp), os = oo * sin(pp);
+    Ray<double> r;
+    r.x = a.pt[0] + a.n1[0] * oc + a.n2[0] * os;
+    r.y = a.pt[1] + a.n1[1] * oc + a.n2[1] * os;
+    r.z = a.pt[2] + a.n1[2] * oc + a.n2[2] * os;
+    r.dx = a.nrm[0]; r.dy = a.nrm[1]; r.dz = a.nrm[2];
+    r.ph = 0.0;
+    r.wl = a.wl;
+    store_ray<T, RTPB_AOS>(static_cast<T*>(a.out), k, 0, r);
+}
+
+// intersect_rays (RT:164-238): closest-approach solve from the first non-singular 2x2 sub-system,
+// verified to 1e-12.  NaN determinants count as "non-zero" exactly like numpy's truthiness.
+struct IsectArgs {
+    const void* __restrict__ r1;
+    const void* __restrict__ r2;
+    void* __restrict__ out;
+    int64_t n, n1, n2;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void intersect_kernel(IsectArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const T* p = static_cast<const T*>(a.r1) + (a.n1 == 1 ? 0 : i) * 8;
+    const T* q = static_cast<const T*>(a.r2) + (a.n2 == 1 ? 0 : i) * 8;
+    const double x1 = p[0], y1 = p[1], z1 = p[2], dx1 = p[3], dy1 = p[4], dz1 = p[5];
+    const double x2 = q[0], y2 = q[1], z2 = q[2], dx2 = q[3], dy2 = q[4], dz2 = q[5];
+    const double nan = qnan<double>();
+    const double det_xz = dx2 * dz1 - dz2 * dx1, det_xy = dx2 * dy1 - dy2 * dx1, det_yz = dz2 * dy1 - dy2 * dz1;
+    double s = nan;
+    if (det_xz != 0.0) s = ((z2 - z1) * dx1 - (x2 - x1) * dz1) / det_xz;
+    else if (det_xy != 0.0) s = ((y2 - y1) * dx1 - (x2 - x1) * dy1) / det_xy;
+    else if (det_yz != 0.0) s = ((y2 - y1) * dz1 - (z2 - z1) * dy1) / det_yz;
+    double t;
+    if (dz1 != 0.0) t = (z2 + s * dz2 - z1) / dz1;
+    else if (dy1 != 0.0) t = (y2 + s * dy2 - y1) / dy1;
+    else t = (x2 + s * dx2 - x1) / dx1;
+    double o[3] = {x1 + t * dx1, y1 + t * dy1, z1 + t * dz1};
+    const double e[3] = {o[0] - (x2 + s * dx2), o[1] - (y2 + s * dy2), o[2] - (z2 + s * dz2)};
+    // numpy.max over the 3 |differences| propagates NaN, and NaN > 1e-12 is false
+    double m = tabs(e[0]);
+    for (int k = 1; k < 3; ++k) {
+        const double v = tabs(e[k]);
+        if (is_nan(m)) break;
+        if (is_nan(v) || v > m) m = v;
+    }
+    if (m > 1e-12) o[0] = o[1] = o[2] = nan;
+    T* out = static_cast<T*>(a.out) + i * 3;
+    out[0] = T(o[0]); out[1] = T(o[1]); out[2] = T(o[2]);
+}
+
+// Spot statistics of one history plane, per contiguous group of `gsize` rays (per
+// (field, wavelength) spot diagrams).  Rays whose x or y is not finite are skipped.  Deterministic:
+// pass 1 reduces each 256-ray tile of a group in a fixed tree order into partials[group][tile];
+// pass 2 sums a group's partials in a fixed order.  Stats: n, Sx, Sy, Sz, Sxx, Syy, Sxy.
+constexpr int kStats = 7;
+struct SpotArgs {
+    const void* __restrict__ plane;
+    double* __restrict__ partials;
+    double* __restrict__ stats;
+    int64_t gsize, ngroups, tiles;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void spot_partial_kernel(SpotArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.y, tile = blockIdx.x;
+    const int64_t j = tile * kBlock + threadIdx.x;
+    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+    if (j < a.gsize) {
+        const T* r = static_cast<const T*>(a.plane) + (g * a.gsize + j) * 8;
+        const double x = r[0], y = r[1], z = r[2];
+        if (x - x == 0.0 && y - y == 0.0) {
+            v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
+        }
+    }
+    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(kBlock) void spot_final_kernel(SpotArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.x;
+    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+    for (int64_t t = threadIdx.x; t < a.tiles; t += kBlock)
+        for (int k = 0; k < kStats; ++k) v[k] += a.partials[(g * a.tiles + t) * kStats + k];
+    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < kStats) a.stats[g * kStats + threadIdx.x] = red[threadIdx.x][0];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------- plans
@@ -802,6 +921,94 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     if (dtype == RTPB_F64) go(double{});
     else if (dtype == RTPB_F32) go(float{});
     else return fail(RTPB_E_INVALID, "bad dtype");
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
+                         int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
+                         void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n_disps <= 0 || nphis <= 0 || !rays_out || !pt || !normal)
+        return fail(RTPB_E_INVALID, "bad collimated-ray arguments");
+    if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    CollArgs a{};
+    a.out = rays_out;
+    a.n_disps = n_disps;
+    a.nphis = nphis;
+    const double* nv = normal;
+    // n1 = (0,1,0) x normal, or normal x (1,0,0) when that vanishes; n2 = normal x n1 (RT:135-144)
+    double n1[3] = {1.0 * nv[2] - 0.0 * nv[1], 0.0 * nv[0] - 0.0 * nv[2], 0.0 * nv[1] - 1.0 * nv[0]};
+    if (std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]) == 0.0) {
+        n1[0] = nv[1] * 0.0 - nv[2] * 0.0;
+        n1[1] = nv[2] * 1.0 - nv[0] * 0.0;
+        n1[2] = nv[0] * 0.0 - nv[1] * 1.0;
+    }
+    const double l1 = std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]);
+    for (double& v : n1) v = v / l1;
+    double n2[3] = {nv[1] * n1[2] - nv[2] * n1[1], nv[2] * n1[0] - nv[0] * n1[2], nv[0] * n1[1] - nv[1] * n1[0]};
+    const double l2 = std::sqrt(n2[0] * n2[0] + n2[1] * n2[1] + n2[2] * n2[2]);
+    for (double& v : n2) v = v / l2;
+    for (int j = 0; j < 3; ++j) {
+        a.pt[j] = pt[j]; a.n1[j] = n1[j]; a.n2[j] = n2[j]; a.nrm[j] = nv[j];
+    }
+    a.start = -displacement_max;
+    a.stop = displacement_max;
+    a.step = n_disps > 1 ? (displacement_max - (-displacement_max)) / double(n_disps - 1) : 0.0;
+    a.phi_start = phi_start;
+    a.wl = wavelength;
+    DeviceGuard g(device);
+    const unsigned blocks = static_cast<unsigned>((n_disps * nphis + kBlock - 1) / kBlock);
+    if (dtype == RTPB_F64)
+        hipLaunchKernelGGL(collimated_kernel<double>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(collimated_kernel<float>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_intersect_rays(int32_t device, int32_t dtype, const void* ray1, int64_t n1, const void* ray2, int64_t n2,
+                        void* pts_out, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    if (n1 < 0 || n2 < 0 || (n1 != n2 && n1 != 1 && n2 != 1))
+        return fail(RTPB_E_INVALID, "ray1 and ray2 must be the same length");
+    const int64_t n = std::max(n1, n2);
+    if (n == 0) return RTPB_OK;
+    if (!ray1 || !ray2 || !pts_out) return fail(RTPB_E_INVALID, "NULL pointer");
+    IsectArgs a{ray1, ray2, pts_out, n, n1, n2};
+    DeviceGuard g(device);
+    const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+    if (dtype == RTPB_F64)
+        hipLaunchKernelGGL(intersect_kernel<double>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(intersect_kernel<float>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t group_size, int64_t n_groups,
+                    double* workspace, int64_t workspace_len, double* stats_out, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    if (group_size <= 0 || n_groups <= 0 || !plane || !stats_out || !workspace)
+        return fail(RTPB_E_INVALID, "bad spot-stats arguments");
+    const int64_t tiles = (group_size + kBlock - 1) / kBlock;
+    if (workspace_len < n_groups * tiles * kStats)
+        return fail(RTPB_E_INVALID, "workspace too small: need n_groups * ceil(group_size/256) * 7 doubles");
+    if (tiles > 65535 * 16384ll || n_groups > 65535) return fail(RTPB_E_LIMIT, "too many groups");
+    SpotArgs a{plane, workspace, stats_out, group_size, n_groups, tiles};
+    DeviceGuard g(device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(n_groups));
+    if (dtype == RTPB_F64) hipLaunchKernelGGL(spot_partial_kernel<double>, grid, dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(spot_partial_kernel<float>, grid, dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
 }

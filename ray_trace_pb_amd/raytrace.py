@@ -90,13 +90,26 @@ def _ray_fan_device(pt, theta_max, n_thetas, wavelength, nphis, center_ray, devi
 
 
 def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: int = 1, phi_start: float = 0.,
-                        normal=(0, 0, 1)) -> np.ndarray:
+                        normal=(0, 0, 1), *, device=None, dtype=None):
     """Parallel rays along ``normal`` through a disk of points around ``pt`` (RT:99-161).
 
     index = idisp*nphis + iphi; position pt + off (n1 cos phi + n2 sin phi) with n1 = y x normal
-    (or normal x x when normal is along y), n2 = normal x n1; offsets linspace(-dmax, dmax, n_disps)."""
+    (or normal x x when normal is along y), n2 = normal x n1; offsets linspace(-dmax, dmax, n_disps).
+    With ``device`` the bundle is generated in HBM by ``rtpb_collimated_rays`` (scalar wavelength)."""
     if np.abs(np.linalg.norm(normal) - 1) > 1e-12:
         raise ValueError("normal must be a normalized vector")
+    if device is not None:
+        import torch
+        dev = torch.device(device)
+        tdt = torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64
+        out = torch.empty((n_disps * nphis, 8), dtype=tdt, device=dev)
+        d3 = C.ctypes.c_double * 3
+        C.check(C.lib().rtpb_collimated_rays(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
+                                             out.data_ptr(), d3(*np.asarray(pt, dtype=float).ravel()),
+                                             float(displacement_max), int(n_disps), int(nphis), float(phi_start),
+                                             d3(*np.asarray(normal, dtype=float).ravel()), float(wavelengths),
+                                             torch.cuda.current_stream(dev).cuda_stream))
+        return out
     phis = np.arange(nphis) * 2 * np.pi / nphis + phi_start
     offs = np.linspace(-displacement_max, displacement_max, n_disps)
     pp, oo = np.meshgrid(phis, offs)
@@ -118,7 +131,10 @@ def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: 
 
 # =============================================================================== ray utilities
 def intersect_rays(ray1, ray2):
-    """Intersection point of pairs of rays (NaN when they do not meet within 1e-12) (RT:164-238)."""
+    """Intersection point of pairs of rays (NaN when they do not meet within 1e-12) (RT:164-238).
+    torch CUDA inputs are solved on the GPU (``rtpb_intersect_rays``) and return a CUDA tensor."""
+    if _is_torch_cuda(ray1) or _is_torch_cuda(ray2):
+        return _intersect_rays_device(ray1, ray2)
     ray1 = np.atleast_2d(ray1)
     ray2 = np.atleast_2d(ray2)
     if len(ray1) == 1 and len(ray2) > 1:
@@ -159,6 +175,22 @@ def intersect_rays(ray1, ray2):
         miss = np.max(np.abs(on1 - on2), axis=1) > 1e-12
         on1[miss] = np.nan
     return on1
+
+
+def _intersect_rays_device(ray1, ray2):
+    import torch
+    dev = ray1.device if _is_torch_cuda(ray1) else ray2.device
+    tdt = ray1.dtype if _is_torch_cuda(ray1) else ray2.dtype
+    r1 = torch.as_tensor(ray1, device=dev).to(tdt).reshape(-1, 8).contiguous()
+    r2 = torch.as_tensor(ray2, device=dev).to(tdt).reshape(-1, 8).contiguous()
+    n1, n2 = r1.shape[0], r2.shape[0]
+    if n1 != n2 and n1 != 1 and n2 != 1:
+        raise ValueError("ray1 and ray2 must be the same length")
+    out = torch.empty((max(n1, n2), 3), dtype=tdt, device=dev)
+    C.check(C.lib().rtpb_intersect_rays(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
+                                        r1.data_ptr(), n1, r2.data_ptr(), n2, out.data_ptr(),
+                                        torch.cuda.current_stream(dev).cuda_stream))
+    return out
 
 
 def propagate_ray2plane(rays, normal, center, material: Material, exclude_backward_propagation: bool = False):

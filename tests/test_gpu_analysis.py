@@ -1,0 +1,91 @@
+"""GPU: device ray generators and device analysis against the reference's
+host semantics (golden vectors) and NumPy."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from ray_trace_pb_amd import analysis  # noqa: E402
+from oracle import rt_numpy as O  # noqa: E402
+from parity import GOLDEN  # noqa: E402
+from serialize import material_to_dict, surface_to_dict  # noqa: E402
+import systems  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("kw", [dict(pt=[0., 1., -2.], dmax=3., n=5, nphis=4, phi_start=0.3, normal=(0, 0, 1)),
+                                dict(pt=[0., 0., 0.], dmax=2., n=4, nphis=3, phi_start=0.,
+                                     normal=(np.sin(0.2), 0, np.cos(0.2))),
+                                dict(pt=[0., 0., 0.], dmax=2., n=3, nphis=2, phi_start=0., normal=(0, 1, 0)),
+                                dict(pt=[1., 2., 3.], dmax=25.4, n=1001, nphis=64, phi_start=0.1, normal=(0, 0, 1))])
+def test_device_collimated_rays_match_host(kw):
+    h = rt.get_collimated_rays(kw["pt"], kw["dmax"], kw["n"], 0.5, nphis=kw["nphis"], phi_start=kw["phi_start"],
+                               normal=kw["normal"])
+    d = rt.get_collimated_rays(kw["pt"], kw["dmax"], kw["n"], 0.5, nphis=kw["nphis"], phi_start=kw["phi_start"],
+                               normal=kw["normal"], device=DEV).cpu().numpy()
+    assert d.shape == h.shape
+    assert np.array_equal(d[:, 3:], h[:, 3:])                  # directions, phase, wavelength exact
+    assert np.allclose(d[:, :3], h[:, :3], rtol=0, atol=4e-15 * max(1.0, kw["dmax"]))   # sin/cos ulps
+
+
+def test_device_intersect_rays_bitwise_vs_reference():
+    g = np.load(os.path.join(GOLDEN, "generators.npz"))
+    got = rt.intersect_rays(torch.from_numpy(g["intersect_in1"]).to(DEV), torch.from_numpy(g["intersect_in2"]).to(DEV))
+    assert np.array_equal(got.cpu().numpy(), g["intersect_out"], equal_nan=True)
+    fan = rt.get_ray_fan([0., 0., 0.], 0.1, 5, 0.5)
+    got = rt.intersect_rays(torch.from_numpy(fan[1]).to(DEV), torch.from_numpy(fan).to(DEV))
+    assert np.array_equal(got.cpu().numpy(), g["intersect_fan_out"], equal_nan=True)
+
+
+def test_device_auto_focus_style_focus_finding():
+    """The reference's focus finder: trace a fan, intersect the traced rays pairwise (RT:832-836)."""
+    system, rays, m0, m1 = systems.c1_plano_convex(rt, mat, nrays=101)
+    h = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
+    got = rt.intersect_rays(h[-1, 51:], h[-1, 50:51])
+    ref = rt.intersect_rays(h[-1, 51:].cpu().numpy(), h[-1, 50:51].cpu().numpy())
+    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+
+
+def test_spot_stats_match_numpy():
+    rng = np.random.default_rng(3)
+    G, per = 7, 1000
+    plane = rng.normal(size=(G * per, 8)) * np.array([1, 2, 3, 1, 1, 1, 1, 1]) + 5.0
+    plane[rng.random(G * per) < 0.1] = np.nan
+    raw = analysis.spot_stats_raw(torch.from_numpy(plane).to(DEV), per).cpu().numpy()
+    p = plane.reshape(G, per, 8)
+    ok = np.isfinite(p[..., 0]) & np.isfinite(p[..., 1])
+    x, y, z = (np.where(ok, p[..., k], 0.0) for k in range(3))
+    ref = np.stack((ok.sum(1), x.sum(1), y.sum(1), z.sum(1), (x * x).sum(1), (y * y).sum(1), (x * y).sum(1)), 1)
+    np.testing.assert_allclose(raw, ref, rtol=1e-12)
+    again = analysis.spot_stats_raw(torch.from_numpy(plane).to(DEV), per).cpu().numpy()
+    assert np.array_equal(raw, again)                          # deterministic reduction
+
+
+def test_spot_sweep_matches_oracle_c5_small():
+    """C5 spot sweep (ODT excitation system) at small size vs the oracle traced on host-built fans."""
+    system = systems.c5_system(rt, mat)
+    fields = systems.c5_field_points(2)
+    wls = [0.405, 0.785]
+    theta, nt, nph = 0.5 * np.pi / 180, 21, 7
+    summ, timing = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields, wls, theta, nt, nph,
+                                       device=DEV, groups_per_batch=3)
+    S = [surface_to_dict(s) for s in system.surfaces]
+    M = [material_to_dict(m) for m in [mat.Constant(1)] + list(system.materials) + [mat.Constant(1)]]
+    raws = []
+    for f in fields:
+        for w in wls:
+            fin = O.ray_trace(S, M, rt.get_ray_fan(f, theta, nt, w, nphis=nph))[-1]
+            ok = np.isfinite(fin[:, 0]) & np.isfinite(fin[:, 1])
+            x, y, z = (np.where(ok, fin[:, k], 0.0) for k in range(3))
+            raws.append([ok.sum(), x.sum(), y.sum(), z.sum(), (x * x).sum(), (y * y).sum(), (x * y).sum()])
+    ref = analysis.summarize(np.array(raws).reshape(len(fields), len(wls), 7))
+    assert np.array_equal(summ["count"], ref["count"])
+    np.testing.assert_allclose(summ["centroid"], ref["centroid"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(summ["rms_radius"], ref["rms_radius"], rtol=1e-6, atol=1e-9)
+    assert timing["rays"] == len(fields) * len(wls) * nt * nph
