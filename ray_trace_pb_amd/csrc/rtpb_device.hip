@@ -185,9 +185,9 @@ __device__ __forceinline__ void gstore(float4* p, const float4& v, bool nt) {
     else *p = v;
 }
 
-template <typename TS, bool NT>
-__device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
-                                                       int64_t n, int lane, const Ray<double>& r) {
+// Stage one record into the wave's tile (XOR-swizzled slots)
+template <typename TS>
+__device__ __forceinline__ void tile_write(uint4* __restrict__ tile, int lane, const Ray<double>& r) {
     if constexpr (sizeof(TS) == 8) {
         const int sw = (lane >> 1) & 3;
         double2* t = reinterpret_cast<double2*>(tile);
@@ -195,7 +195,23 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
         t[4 * lane + (1 ^ sw)] = make_double2(r.z, r.dx);
         t[4 * lane + (2 ^ sw)] = make_double2(r.dy, r.dz);
         t[4 * lane + (3 ^ sw)] = make_double2(r.ph, r.wl);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+        const int sw = (lane >> 2) & 1;
+        float4* t = reinterpret_cast<float4*>(tile);
+        t[2 * lane + (0 ^ sw)] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
+        t[2 * lane + (1 ^ sw)] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
+    }
+}
+
+// Write the wave's staged block (64 records) to `plane` lane-contiguously: 1 KiB per store instruction.
+// Callers wait for the tile writes first (lgkmcnt(0)); the compiler waits for the tile reads before the
+// global stores that consume them, and a wave's DS operations execute in order, so the next tile_write
+// cannot overtake these reads.
+template <typename TS, bool NT>
+__device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
+                                           int64_t n, int lane) {
+    if constexpr (sizeof(TS) == 8) {
+        const double2* t = reinterpret_cast<const double2*>(tile);
         const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
         double2* g = reinterpret_cast<double2*>(plane + ray0 * 8);
 #pragma unroll
@@ -205,11 +221,7 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
             if (c < nchunks) gstore(g + c, v, NT);
         }
     } else {
-        const int sw = (lane >> 2) & 1;
-        float4* t = reinterpret_cast<float4*>(tile);
-        t[2 * lane + (0 ^ sw)] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
-        t[2 * lane + (1 ^ sw)] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float4* t = reinterpret_cast<const float4*>(tile);
         const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
         float4* g = reinterpret_cast<float4*>(plane + ray0 * 8);
 #pragma unroll
@@ -219,8 +231,9 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
             if (c < nchunks) gstore(g + c, v, NT);
         }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
 // TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
@@ -228,7 +241,9 @@ __device__ __forceinline__ void store_plane_aos_staged(uint4* __restrict__ tile,
 template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void trace_kernel(TraceArgs<TS> a) {
     using T = double;
-    __shared__ uint4 tiles[kWaves][kTileBytes / 16];
+    constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
+    constexpr bool kNT = (STORE & 2) != 0;
+    __shared__ uint4 tiles[kWaves][2][kTileBytes / 16];  // two tiles per wave: "at" and "after" planes
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int64_t ray0 = i - lane;                       // first ray of this wave
@@ -237,17 +252,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     Ray<T> r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
     const T wl0 = r.wl;
     TS* __restrict__ out = a.out;
-    uint4* tile = tiles[threadIdx.x >> 6];
-    auto put = [&](int64_t off, const Ray<T>& q) {
-        if constexpr ((STORE & 1) && OUT_LAYOUT == RTPB_AOS) {
-            store_plane_aos_staged<TS, (STORE & 2) != 0>(tile, out + off, ray0, a.n, lane, q);
-        } else {
-            if (valid) store_ray<TS, OUT_LAYOUT>(out + off, i, a.out_fs, q);
-        }
-    };
+    uint4* tile_a = tiles[threadIdx.x >> 6][0];
+    uint4* tile_b = tiles[threadIdx.x >> 6][1];
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
-        put(slot_off, r);
+        if constexpr (kStaged) {
+            tile_write<TS>(tile_a, lane, r);
+            lds_wait();
+            tile_flush<TS, kNT>(tile_a, out, ray0, a.n, lane);
+        } else if (valid) {
+            store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
+        }
         slot_off += a.out_ps;
     }
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
@@ -259,13 +274,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
         Ray<T> at, after;
         propagate_surface<T>(load_surface<T>(surf + s), r, n_cur, n_next, at, after);
         const int p = 2 * s + 1;
-        if (plane_bit(a.mask_lo, a.mask_hi, p)) {
-            put(slot_off, at);
-            slot_off += a.out_ps;
-        }
-        if (plane_bit(a.mask_lo, a.mask_hi, p + 1)) {
-            put(slot_off, after);
-            slot_off += a.out_ps;
+        const bool st_at = plane_bit(a.mask_lo, a.mask_hi, p);          // wave-uniform
+        const bool st_after = plane_bit(a.mask_lo, a.mask_hi, p + 1);
+        const int64_t off_at = slot_off;
+        slot_off += st_at ? a.out_ps : 0;
+        const int64_t off_after = slot_off;
+        slot_off += st_after ? a.out_ps : 0;
+        if constexpr (kStaged) {
+            // both planes of the surface share one LDS round trip
+            if (st_at) tile_write<TS>(tile_a, lane, at);
+            if (st_after) tile_write<TS>(tile_b, lane, after);
+            if (st_at || st_after) lds_wait();
+            if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
+            if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
+        } else if (valid) {
+            if (st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
+            if (st_after) store_ray<TS, OUT_LAYOUT>(out + off_after, i, a.out_fs, after);
         }
         r = after;
         n_cur = n_next;
@@ -540,7 +564,6 @@ hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
     if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
         const int w = g_waves_per_eu.load();
         if (w == 5) return launch_w<T, IL, OL, ST, 5>(a, st);
-        if (w == 6) return launch_w<T, IL, OL, ST, 6>(a, st);
     }
     return launch_w<T, IL, OL, ST, 1>(a, st);
 }
@@ -1024,7 +1047,7 @@ int rtpb_set_tuning(const char* key, int64_t value) {
         return RTPB_OK;
     }
     if (std::strcmp(key, "waves_per_eu") == 0) {
-        if (value != 0 && value != 5 && value != 6) return fail(RTPB_E_INVALID, "waves_per_eu must be 0, 5 or 6");
+        if (value != 0 && value != 5) return fail(RTPB_E_INVALID, "waves_per_eu must be 0 or 5");
         g_waves_per_eu.store(static_cast<int>(value));
         return RTPB_OK;
     }

@@ -47,14 +47,14 @@ def main():
             x = torch.from_numpy(rays_np).to(dev, dtype=tdt)
             for planes in ("all", "final"):
                 sel = E.resolve_planes(planes, S)
-                for layout in ("aos", "aos-nt", "aos-nt-w5", "aos-nt-w6", "aos-direct", "soa"):
+                for layout in ("aos", "aos-nt", "aos-nt-w5", "aos-direct", "soa"):
                     lc = C.RTPB_SOA if layout == "soa" else C.RTPB_AOS
                     shape = (len(sel), n, 8) if lc == C.RTPB_AOS else (len(sel), 8, n)
                     out = torch.empty(shape, dtype=tdt, device=dev)
                     w = 8 if dtype == "f64" else 4
                     nbytes = n * 8 * w * (1 + len(sel))
                     name = f"{cfg}/{dtype}/{planes}/{layout}"
-                    mode = {"aos": 1, "aos-nt": 3, "aos-nt-w5": 3 + 5 * 4, "aos-nt-w6": 3 + 6 * 4, "aos-direct": 0,
+                    mode = {"aos": 1, "aos-nt": 3, "aos-nt-w5": 3 + 5 * 4, "aos-direct": 0,
                             "soa": 0}[layout]
                     variants.append((name, low, x, sel, lc, out, nbytes, n * S, mode))
     if args.only:
