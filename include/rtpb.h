@@ -166,6 +166,8 @@ int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t gr
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.
    "nt_stores": 1 (default) = non-temporal global stores for the staged AOS tiles (the history is
    streamed out and never re-read by the kernel); 0 = default cache policy.
+   "stage_input": 1 = also load AOS input records through the LDS tile (1 KiB per load instruction);
+   0 (default) = 4 x 16-byte loads per lane.
    "waves_per_eu": 0 (default: compiler choice, 4 waves/SIMD) or 5 = occupancy target for the
    AOS->AOS staged kernel (the compiler then spills to scratch to fit). */
 int rtpb_set_tuning(const char* key, int64_t value);

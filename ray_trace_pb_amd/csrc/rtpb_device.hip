@@ -235,6 +235,45 @@ __device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* _
 
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Inverse of tile_flush for the input: lane l loads 16-byte chunks l, l+64, ... of the wave's contiguous
+// record block (1 KiB per load instruction) into the tile, then reads back its own record.
+template <typename TS>
+__device__ __forceinline__ Ray<double> tile_load(uint4* __restrict__ tile, const TS* __restrict__ in, int64_t ray0,
+                                                 int64_t n, int lane) {
+    Ray<double> r;
+    if constexpr (sizeof(TS) == 8) {
+        double2* t = reinterpret_cast<double2*>(tile);
+        const double2* g = reinterpret_cast<const double2*>(in + ray0 * 8);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
+            const double2 v = g[c < nchunks ? c : nchunks - 4 + pp];      // tail lanes re-read the last ray
+            t[4 * rr + (pp ^ ((rr >> 1) & 3))] = v;
+        }
+        lds_wait();
+        const int sw = (lane >> 1) & 3;
+        const double2 a = t[4 * lane + (0 ^ sw)], b = t[4 * lane + (1 ^ sw)], c = t[4 * lane + (2 ^ sw)],
+                      d = t[4 * lane + (3 ^ sw)];
+        r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
+    } else {
+        float4* t = reinterpret_cast<float4*>(tile);
+        const float4* g = reinterpret_cast<const float4*>(in + ray0 * 8);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
+            const float4 v = g[c < nchunks ? c : nchunks - 2 + pp];
+            t[2 * rr + (pp ^ ((rr >> 2) & 1))] = v;
+        }
+        lds_wait();
+        const int sw = (lane >> 2) & 1;
+        const float4 a = t[2 * lane + (0 ^ sw)], b = t[2 * lane + (1 ^ sw)];
+        r.x = a.x; r.y = a.y; r.z = a.z; r.dx = a.w; r.dy = b.x; r.dz = b.y; r.ph = b.z; r.wl = b.w;
+    }
+    return r;
+}
+
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
 // TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
 // global stores for the staged tiles.
@@ -249,11 +288,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     const int64_t ray0 = i - lane;                       // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
     const bool valid = i < a.n;
-    Ray<T> r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
-    const T wl0 = r.wl;
-    TS* __restrict__ out = a.out;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
     uint4* tile_b = tiles[threadIdx.x >> 6][1];
+    Ray<T> r;
+    if constexpr (kStaged && IN_LAYOUT == RTPB_AOS && (STORE & 4)) r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
+    else r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
+    const T wl0 = r.wl;
+    TS* __restrict__ out = a.out;
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
         if constexpr (kStaged) {
@@ -551,6 +592,7 @@ thread_local TimingState g_timing;
 std::atomic<int> g_aos_staging{1};
 std::atomic<int> g_nt_stores{1};
 std::atomic<int> g_waves_per_eu{0};
+std::atomic<int> g_stage_input{0};
 
 template <typename T, int IL, int OL, int ST, int W>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
@@ -575,6 +617,7 @@ hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, hipStream_t st) {
     if (ol == RTPB_AOS) {
         if (!staged)
             return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 0>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 0>(a, st);
+        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<T, RTPB_AOS, RTPB_AOS, 7>(a, st);
         if (nt)
             return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 3>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 3>(a, st);
         return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 1>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 1>(a, st);
@@ -1044,6 +1087,10 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     }
     if (std::strcmp(key, "nt_stores") == 0) {
         g_nt_stores.store(value != 0);
+        return RTPB_OK;
+    }
+    if (std::strcmp(key, "stage_input") == 0) {
+        g_stage_input.store(value != 0);
         return RTPB_OK;
     }
     if (std::strcmp(key, "waves_per_eu") == 0) {

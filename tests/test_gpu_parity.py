@@ -117,6 +117,22 @@ def test_soa_layout_matches_aos():
     assert np.array_equal(soa.transpose(1, 2).cpu().numpy(), ref, equal_nan=True)
 
 
+@pytest.mark.parametrize("knob", [("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1), ("waves_per_eu", 5)])
+def test_tuning_variants_bitwise(knob):
+    """Every store/load strategy is a pure data-movement change: bit-identical histories."""
+    system, m0, m1, rays, ref = build_case("stress")
+    lib = C.lib()
+    default = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0}[knob[0]]
+    C.check(lib.rtpb_set_tuning(knob[0].encode(), knob[1]))
+    try:
+        for dt, r in (("float64", rays), ("float32", rays.astype(np.float32))):
+            got = system.ray_trace(torch.from_numpy(r).to(DEV), m0, m1, dtype=dt).cpu().numpy()
+            exp = ref if dt == "float64" else oracle(system, m0, m1, r.astype(np.float64)).astype(np.float32)
+            assert np.array_equal(got, exp, equal_nan=True), (knob, dt)
+    finally:
+        C.check(lib.rtpb_set_tuning(knob[0].encode(), default))
+
+
 def test_sharded_host_trace_is_bitwise_equal():
     """Ray sharding over devices (here: two shards on GPU 0) gives exactly the unsharded history."""
     system, m0, m1, rays, ref = build_case("stress")

@@ -47,14 +47,14 @@ def main():
             x = torch.from_numpy(rays_np).to(dev, dtype=tdt)
             for planes in ("all", "final"):
                 sel = E.resolve_planes(planes, S)
-                for layout in ("aos", "aos-nt", "aos-nt-w5", "aos-direct", "soa"):
+                for layout in ("aos", "aos-nt", "aos-nt-sin", "aos-nt-w5", "aos-direct", "soa"):
                     lc = C.RTPB_SOA if layout == "soa" else C.RTPB_AOS
                     shape = (len(sel), n, 8) if lc == C.RTPB_AOS else (len(sel), 8, n)
                     out = torch.empty(shape, dtype=tdt, device=dev)
                     w = 8 if dtype == "f64" else 4
                     nbytes = n * 8 * w * (1 + len(sel))
                     name = f"{cfg}/{dtype}/{planes}/{layout}"
-                    mode = {"aos": 1, "aos-nt": 3, "aos-nt-w5": 3 + 5 * 4, "aos-direct": 0,
+                    mode = {"aos": 1, "aos-nt": 3, "aos-nt-w5": 3 + 5 * 4, "aos-nt-sin": 3 + 64, "aos-direct": 0,
                             "soa": 0}[layout]
                     variants.append((name, low, x, sel, lc, out, nbytes, n * S, mode))
     if args.only:
@@ -65,11 +65,15 @@ def main():
     dst = torch.empty_like(src)
     times = {v[0]: [] for v in variants}
     times["copy_768MB"] = []
+    rng = np.random.default_rng(0)
     for _ in range(args.rounds):
-        for name, low, x, sel, lc, out, nbytes, units, staged in variants:
+        order = rng.permutation(len(variants))          # randomise the order every round
+        for vi in order:
+            name, low, x, sel, lc, out, nbytes, units, staged = variants[vi]
             C.check(lib.rtpb_set_tuning(b"aos_staging", staged & 1))
             C.check(lib.rtpb_set_tuning(b"nt_stores", (staged >> 1) & 1))
-            C.check(lib.rtpb_set_tuning(b"waves_per_eu", staged >> 2))
+            C.check(lib.rtpb_set_tuning(b"waves_per_eu", (staged >> 2) & 15))
+            C.check(lib.rtpb_set_tuning(b"stage_input", staged >> 6))
             E.trace_device(low, x, sel, layout_out=lc, out=out)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
@@ -90,9 +94,11 @@ def main():
     C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
     C.check(lib.rtpb_set_tuning(b"nt_stores", 1))
     C.check(lib.rtpb_set_tuning(b"waves_per_eu", 0))
+    C.check(lib.rtpb_set_tuning(b"stage_input", 0))
     for name, low, x, sel, lc, out, nbytes, units, staged in variants:
         ms = float(np.median(times[name]))
-        res[name] = {"ms": ms, "GBps": nbytes / ms / 1e6, "ray_surf_per_s": units / ms * 1e3}
+        res[name] = {"ms": ms, "ms_min": float(np.min(times[name])), "GBps": nbytes / ms / 1e6,
+                     "ray_surf_per_s": units / ms * 1e3}
     ms = float(np.median(times["copy_768MB"]))
     res["copy_768MB"] = {"ms": ms, "GBps": 2 * src.numel() * 8 / ms / 1e6}
     for k, v in res.items():
