@@ -148,6 +148,15 @@ int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const do
                          int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
                          void* stream);
 
+/* propagate_ray2plane(rays, normal, center, material, exclude_backward_propagation) (RT:241-306) on
+   device rays (AOS n x 8).  normal / center: DEVICE pointers to 3 doubles (broadcast) or n x 3 doubles
+   (*_per_ray = 1).  ts_out (device, n doubles) may be NULL.  workspace: device bytes for the material
+   descriptor (>= 256 + 16 * max(table_len, 1)); the call synchronises `stream` after staging it. */
+int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int64_t n_rays, const double* normal,
+                         int32_t normal_per_ray, const double* center, int32_t center_per_ray,
+                         const rtpb_material* material, int32_t exclude_backward, void* rays_out, double* ts_out,
+                         void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- device analysis ------------------------------------------------------------------------- */
 /* intersect_rays(ray1, ray2) (RT:164-238) on device rays (AOS, n x 8; a length-1 side broadcasts).
    pts_out: max(n1, n2) x 3 intersection points, NaN where the rays do not meet within 1e-12. */

@@ -54,6 +54,8 @@ SIGNATURES = {
     "rtpb_collimated_rays": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, _dbl,
                                             ctypes.POINTER(_dbl), _dbl, _P]),
     "rtpb_intersect_rays": (ctypes.c_int, [_i32, _i32, _P, _i64, _P, _i64, _P, _P]),
+    "rtpb_propagate_plane": (ctypes.c_int, [_i32, _i32, _P, _i64, _P, _i32, _P, _i32, ctypes.POINTER(Material), _i32,
+                                            _P, _P, _P, _i64, _P]),
     "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),
     "rtpb_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "rtpb_timing_enable": (ctypes.c_int, [_i32]),

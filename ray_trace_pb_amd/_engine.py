@@ -89,6 +89,24 @@ def lower(surfaces, materials, wavelengths, dtype):
     return low
 
 
+def lower_material(m, wavelengths):
+    """One ``rtpb_material`` (tables keep a reference on the returned struct as ``_keep``)."""
+    d = C.Material()
+    lowered = m._rtpb_lower() if hasattr(m, "_rtpb_lower") else None
+    if lowered is not None:
+        d.kind, coeffs = lowered
+        d.c[:] = [float(c) for c in coeffs]
+        return d
+    wl = np.asarray(wavelengths(), dtype=np.float64)
+    nv = np.broadcast_to(np.asarray(m.n(wl), dtype=np.float64), wl.shape)
+    tab = np.ascontiguousarray(np.stack((wl, nv), axis=1).ravel())
+    d.kind = C.RTPB_TABLE
+    d.table_len = wl.size
+    d.table = tab.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    d._keep = tab
+    return d
+
+
 # ------------------------------------------------------------------------- plan cache
 _PLANS = collections.OrderedDict()
 _PLANS_MAX = 32

@@ -485,6 +485,36 @@ __global__ __launch_bounds__(kBlock) void spot_final_kernel(SpotArgs a) {
     if (threadIdx.x < kStats) a.stats[g * kStats + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// propagate_ray2plane (RT:241-306) as a standalone operation: per-ray or broadcast plane normal/center,
+// material n(lambda) from a lowered descriptor, optional exclusion of backward propagation; also
+// returns the propagation parameter t.
+struct PlaneArgs {
+    const void* __restrict__ in;
+    void* __restrict__ out;
+    double* __restrict__ ts;
+    const double* __restrict__ nrm;   // 3 or 3*n doubles
+    const double* __restrict__ ctr;
+    const DevMaterial<double>* __restrict__ mat;
+    const double* __restrict__ table;
+    int64_t n;
+    int32_t nrm_per_ray, ctr_per_ray, exclude;
+};
+
+template <typename TS>
+__global__ __launch_bounds__(kBlock) void plane_kernel(PlaneArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.in), i, 0);
+    const double* nv = a.nrm + (a.nrm_per_ray ? 3 * i : 0);
+    const double* cv = a.ctr + (a.ctr_per_ray ? 3 * i : 0);
+    DevMaterial<double> m = *a.mat;
+    const double n = material_n<double>(m, r.wl, a.table);
+    double t;
+    const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0, &t);
+    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, o);
+    if (a.ts) a.ts[i] = t;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------- plans
@@ -1075,6 +1105,62 @@ int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t gr
     else hipLaunchKernelGGL(spot_partial_kernel<float>, grid, dim3(kBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int64_t n_rays, const double* normal,
+                         int32_t normal_per_ray, const double* center, int32_t center_per_ray,
+                         const rtpb_material* material, int32_t exclude_backward, void* rays_out, double* ts_out,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    if (n_rays < 0 || !material || !normal || !center) return fail(RTPB_E_INVALID, "bad propagate-plane arguments");
+    if (n_rays == 0) return RTPB_OK;
+    if (!rays_in || !rays_out) return fail(RTPB_E_INVALID, "NULL ray buffer");
+    if ((reinterpret_cast<uintptr_t>(rays_in) | reinterpret_cast<uintptr_t>(rays_out)) % 16)
+        return fail(RTPB_E_INVALID, "ray buffers must be 16-byte aligned");
+    if (material->kind < RTPB_CONSTANT || material->kind > RTPB_TABLE) return fail(RTPB_E_INVALID, "bad material kind");
+    const int64_t ntab = material->kind == RTPB_TABLE ? material->table_len : 0;
+    if (material->kind == RTPB_TABLE && (ntab <= 0 || !material->table))
+        return fail(RTPB_E_INVALID, "empty material table");
+    // workspace (device): [DevMaterial<double>][table pairs], staged with one async H2D copy
+    const size_t need = align256(sizeof(DevMaterial<double>)) + size_t(2 * std::max<int64_t>(ntab, 1)) * sizeof(double);
+    if (!workspace || workspace_bytes < static_cast<int64_t>(need))
+        return fail(RTPB_E_INVALID, "workspace too small (need " + std::to_string(need) + " bytes)");
+    std::vector<unsigned char> host(need, 0);
+    DevMaterial<double> dm{};
+    dm.kind = material->kind;
+    bool zero = material->kind == RTPB_SELLMEIER;
+    for (int j = 0; j < 6; ++j) {
+        dm.c[j] = material->c[j];
+        zero = zero && material->c[j] == 0.0;
+    }
+    if (zero) dm.kind = VACUUM;
+    dm.table_off = 0;
+    dm.table_len = static_cast<int32_t>(ntab);
+    std::memcpy(host.data(), &dm, sizeof(dm));
+    if (ntab) std::memcpy(host.data() + align256(sizeof(dm)), material->table, size_t(2 * ntab) * sizeof(double));
+    DeviceGuard g(device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(workspace, host.data(), need, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));      // `host` is a pageable temporary
+    PlaneArgs a{};
+    a.in = rays_in;
+    a.out = rays_out;
+    a.ts = ts_out;
+    a.nrm = normal;
+    a.ctr = center;
+    a.mat = reinterpret_cast<const DevMaterial<double>*>(workspace);
+    a.table = reinterpret_cast<const double*>(static_cast<char*>(workspace) + align256(sizeof(dm)));
+    a.n = n_rays;
+    a.nrm_per_ray = normal_per_ray;
+    a.ctr_per_ray = center_per_ray;
+    a.exclude = exclude_backward;
+    const unsigned blocks = static_cast<unsigned>((n_rays + kBlock - 1) / kBlock);
+    if (dtype == RTPB_F64) hipLaunchKernelGGL(plane_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(plane_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
 }

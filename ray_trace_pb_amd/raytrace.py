@@ -198,26 +198,38 @@ def propagate_ray2plane(rays, normal, center, material: Material, exclude_backwa
 
     Returns ``(rays_out, ts)``; the phase grows by |d t| sign(t) 2 pi / wavelength n(wavelength); rays
     that must travel backwards become NaN when ``exclude_backward_propagation``.  ``normal`` and
-    ``center`` broadcast against (N, 3)."""
-    rays = np.atleast_2d(np.array(rays, copy=True))
-    normal = np.atleast_2d(np.asarray(normal).squeeze())
-    center = np.atleast_2d(np.asarray(center).squeeze())
-    p, d = rays[:, 0:3], rays[:, 3:6]
-    wls = rays[:, 7]
-    nx, ny, nz = normal[:, 0], normal[:, 1], normal[:, 2]
-    ts = -((p[:, 0] - center[:, 0]) * nx + (p[:, 1] - center[:, 1]) * ny + (p[:, 2] - center[:, 2]) * nz) / \
-        (d[:, 0] * nx + d[:, 1] * ny + d[:, 2] * nz)
-    with np.errstate(invalid="ignore"):
-        sgn = np.where(ts < 0, -1, 1)
-    step = d * ts[:, None]
-    out = np.empty_like(rays)
-    out[:, 0:3] = p + step
-    out[:, 3:6] = d
-    out[:, 6] = rays[:, 6] + np.linalg.norm(step, axis=1) * sgn * 2 * np.pi / wls * material.n(wls)
-    out[:, 7] = wls
-    if exclude_backward_propagation:
-        out[sgn == -1, :] = np.nan
-    return out, ts
+    ``center`` broadcast against (N, 3).  Runs on the GPU (``rtpb_propagate_plane``, the same
+    arithmetic as the fused trace kernel): NumPy in -> NumPy out (float64), torch CUDA in -> torch out."""
+    import torch
+    on_device = _is_torch_cuda(rays)
+    dev = rays.device if on_device else torch.device("cuda", torch.cuda.current_device())
+    r = (rays if on_device else torch.from_numpy(np.atleast_2d(np.asarray(rays, dtype=np.float64)))).to(
+        dev, dtype=torch.float64)
+    r = r.reshape(-1, 8).contiguous()
+    n = r.shape[0]
+
+    def plane_vec(v):
+        a = np.asarray(v.cpu() if _is_torch_cuda(v) else v, dtype=np.float64).squeeze()
+        if a.ndim == 1 and a.size == 3:
+            return torch.from_numpy(a.copy()).to(dev), 0
+        a = a.reshape(-1, 3)
+        if a.shape[0] != n:
+            raise ValueError("normal and center must broadcast to (N, 3)")
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev), 1
+
+    nv, n_per = plane_vec(normal)
+    cv, c_per = plane_vec(center)
+    low = E.lower_material(material, lambda: torch.unique(r[:, 7]).cpu().numpy())
+    ws = torch.empty(256 + 16 * max(low.table_len, 1), dtype=torch.uint8, device=dev)
+    out = torch.empty_like(r)
+    ts = torch.empty(n, dtype=torch.float64, device=dev)
+    C.check(C.lib().rtpb_propagate_plane(dev.index or 0, C.RTPB_F64, r.data_ptr(), n, nv.data_ptr(), n_per,
+                                         cv.data_ptr(), c_per, C.ctypes.byref(low), int(bool(exclude_backward_propagation)),
+                                         out.data_ptr(), ts.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         torch.cuda.current_stream(dev).cuda_stream))
+    if on_device:
+        return out, ts
+    return out.cpu().numpy(), ts.cpu().numpy()
 
 
 def ray_angle_about_axis(rays, reference_axis):

@@ -78,8 +78,6 @@ def test_generators_and_utilities_match_reference():
     assert np.array_equal(rt.intersect_rays(fan[1], fan), g["intersect_fan_out"], equal_nan=True)
     ang, na = rt.ray_angle_about_axis(g["intersect_in1"], np.array([0., 0., 1.]))
     assert np.array_equal(ang, g["angle_out"], equal_nan=True) and np.array_equal(na, g["angle_na"], equal_nan=True)
-    dist, near = rt.dist_pt2plane(g["intersect_in1"][:, :3], np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))
-    assert np.array_equal(dist, g["dist_out"], equal_nan=True) and np.array_equal(near, g["dist_near"], equal_nan=True)
 
 
 def test_generator_argument_errors():

@@ -89,3 +89,34 @@ def test_spot_sweep_matches_oracle_c5_small():
     np.testing.assert_allclose(summ["centroid"], ref["centroid"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(summ["rms_radius"], ref["rms_radius"], rtol=1e-6, atol=1e-9)
     assert timing["rays"] == len(fields) * len(wls) * nt * nph
+
+
+def test_dist_pt2plane_bitwise_vs_reference():
+    g = np.load(os.path.join(GOLDEN, "generators.npz"))
+    dist, near = rt.dist_pt2plane(g["intersect_in1"][:, :3], np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))
+    assert np.array_equal(dist, g["dist_out"], equal_nan=True)
+    assert np.array_equal(near, g["dist_near"], equal_nan=True)
+
+
+@pytest.mark.parametrize("exclude", [False, True])
+def test_propagate_ray2plane_device_bitwise_vs_oracle(exclude):
+    """Per-ray planes (the PerfectLens front-focal-plane case, RT:1693) and broadcast planes; a user
+    Material subclass goes through the wavelength table."""
+    rays = systems.stress_rays(3000, seed=11)
+    rng = np.random.default_rng(2)
+    nrm = rng.normal(size=(3000, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    ctr = rng.normal(size=(3000, 3)) * 5
+    Cauchy = systems.cauchy_class(mat)
+    for m, md in ((mat.Bk7(), material_to_dict(mat.Bk7())), (mat.Constant(1.4), {"type": "Constant", "n": 1.4}),
+                  (Cauchy(), {"type": "Cauchy", "a": 1.5046, "b": 0.0042})):
+        for nv, cv in ((nrm, ctr), (np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))):
+            got, ts = rt.propagate_ray2plane(rays, nv, cv, m, exclude_backward_propagation=exclude)
+            R = O.Rays.from_array(rays)
+            nn = tuple(nv[:, k] for k in range(3)) if nv.ndim == 2 else tuple(nv)
+            cc = tuple(cv[:, k] for k in range(3)) if cv.ndim == 2 else tuple(cv)
+            ref, tref = O.to_plane(R, nn, cc, O.refractive_index(md, R.wl), exclude)
+            assert np.array_equal(got, ref.to_array(), equal_nan=True)
+            assert np.array_equal(ts, tref, equal_nan=True)
+    t_out, t_ts = rt.propagate_ray2plane(torch.from_numpy(rays).to(DEV), nrm, ctr, mat.Bk7())
+    assert t_out.is_cuda and t_ts.is_cuda
