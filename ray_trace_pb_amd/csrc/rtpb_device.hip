@@ -746,6 +746,8 @@ int stage_reserve(HostStage& hs, size_t in_bytes, size_t out_bytes) {
 void parallel_scatter(char* out, const char* staged, int nslots, int64_t slot_stride_bytes, int64_t piece_bytes,
                       int T) {
     const int64_t total = piece_bytes * nslots;
+    // a thread per >= 8 MiB: spawning threads costs ~10-20 us each, a small scatter is one memcpy
+    T = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(T, total >> 23)));
     const int64_t per = (total + T - 1) / T;
     auto job = [&](int t) {
         int64_t lo = t * per, hi = std::min<int64_t>(total, lo + per);
