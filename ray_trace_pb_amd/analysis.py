@@ -99,3 +99,43 @@ def _fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray, code)
     C.check(C.lib().rtpb_ray_fan(buf.device.index or 0, code, buf.data_ptr(), d3(*np.asarray(pt, dtype=float).ravel()),
                                  float(theta_max), int(n_thetas), int(nphis), d3(*np.asarray(center_ray, dtype=float)),
                                  float(wavelength), torch.cuda.current_stream(buf.device).cuda_stream))
+
+
+def pupil_psf(system, initial_material, final_material, source_points, wavelength, theta_max, n_thetas, nphis,
+              pupil_plane, pupil_radius, grid_step, grid_extent=3.0, device="cuda:0"):
+    """Point-spread functions from pupil phases (the pipeline of
+    scripts/2022_02_06_perfect_imaging_system_psf.py:73-105).
+
+    For every source point: a ``get_ray_fan(src, theta_max, n_thetas, wavelength, nphis)`` is generated
+    and traced on the GPU (only history plane ``pupil_plane`` is stored); the pupil phase (column 6)
+    is interpolated onto a square grid of pitch ``grid_step`` spanning +-grid_extent*pupil_radius with
+    ``scipy.interpolate.griddata`` (linear, Delaunay -- as the script; host), masked outside
+    ``pupil_radius`` and where undefined, and Fourier transformed on the GPU (torch.fft = hipFFT):
+    E_out = fftshift(fft2(ifftshift(exp(i phi)))).  Returns (psf |E_out|^2 normalised to the stack
+    maximum, pupil field, grid coordinates)."""
+    import torch
+    from scipy.interpolate import griddata
+    from .raytrace import get_ray_fan
+    dev = torch.device(device)
+    src = np.atleast_2d(np.asarray(source_points, dtype=float))
+    nxy = int(2 * (grid_extent * pupil_radius // grid_step) + 1)
+    xs = grid_step * np.arange(nxy)
+    xs -= np.mean(xs)
+    xx, yy = np.meshgrid(xs, xs)
+    interp_pts = np.stack((xx.ravel(), yy.ravel()), axis=1)
+    outside = np.sqrt(xx ** 2 + yy ** 2) > pupil_radius
+    pupil = np.zeros((len(src), nxy, nxy), dtype=complex)
+    for ii, p in enumerate(src):
+        rays = get_ray_fan(p, theta_max, n_thetas, wavelength, nphis=nphis, device=dev)
+        plane = system.ray_trace(rays, initial_material, final_material, planes=[pupil_plane])[0]
+        h = plane.cpu().numpy()
+        ok = ~np.isnan(h[:, 0]) & ~np.isnan(h[:, 1])
+        phis = griddata(h[ok, :2], h[ok, 6], interp_pts).reshape(xx.shape)
+        e = np.exp(1j * phis)
+        e[outside] = 0
+        e[np.isnan(phis)] = 0
+        pupil[ii] = e
+    pt = torch.from_numpy(pupil).to(dev)
+    out = torch.fft.fftshift(torch.fft.fft2(torch.fft.ifftshift(pt, dim=(-2, -1))), dim=(-2, -1))
+    psf = (out.abs() ** 2).cpu().numpy()
+    return psf / psf.max(), pupil, xs

@@ -120,3 +120,37 @@ def test_propagate_ray2plane_device_bitwise_vs_oracle(exclude):
             assert np.array_equal(ts, tref, equal_nan=True)
     t_out, t_ts = rt.propagate_ray2plane(torch.from_numpy(rays).to(DEV), nrm, ctr, mat.Bk7())
     assert t_out.is_cuda and t_ts.is_cuda
+
+
+def test_pupil_psf_matches_host_pipeline():
+    """§8f #4: GPU trace + griddata + GPU FFT vs the reference script's NumPy pipeline on the oracle."""
+    from numpy import fft
+    from scipy.interpolate import griddata
+    wavelength, n1, na, mag, ftl = 532e-6, 1.4, 1.35, 100, 200
+    alpha = np.arcsin(na / n1)
+    f1 = ftl / mag
+    r1 = na * f1
+    system = rt.System([rt.PerfectLens(f1, [0, 0, n1 * f1], [0, 0, 1], alpha),
+                        rt.FlatSurface([0, 0, n1 * f1 + f1], [0, 0, 1], 4 * r1),
+                        rt.PerfectLens(ftl, [0, 0, n1 * f1 + f1 + ftl], [0, 0, 1], na / mag),
+                        rt.FlatSurface([0, 0, n1 * f1 + f1 + 2 * ftl], [0, 0, 1], r1)],
+                       [mat.Vacuum(), mat.Vacuum(), mat.Vacuum()])
+    srcs = [[0, 0, -1e-4], [0, 0, 0], [0, 0, 1e-4]]
+    psf, pupil, xs = analysis.pupil_psf(system, mat.Constant(n1), mat.Vacuum(), srcs, wavelength, alpha, 41, 21,
+                                        pupil_plane=4, pupil_radius=r1, grid_step=0.05, device=DEV)
+    S = [surface_to_dict(s) for s in system.surfaces]
+    M = [material_to_dict(m) for m in [mat.Constant(n1)] + list(system.materials) + [mat.Vacuum()]]
+    xx, yy = np.meshgrid(xs, xs)
+    ref = []
+    for p in srcs:
+        h = O.ray_trace(S, M, rt.get_ray_fan(p, alpha, 41, wavelength, nphis=21))[4]
+        ok = ~np.isnan(h[:, 0]) & ~np.isnan(h[:, 1])
+        ph = griddata(h[ok, :2], h[ok, 6], np.stack((xx.ravel(), yy.ravel()), 1)).reshape(xx.shape)
+        e = np.exp(1j * ph)
+        e[np.sqrt(xx ** 2 + yy ** 2) > r1] = 0
+        e[np.isnan(ph)] = 0
+        ref.append(np.abs(fft.fftshift(fft.fft2(fft.ifftshift(e)))) ** 2)
+    ref = np.array(ref)
+    ref /= ref.max()
+    np.testing.assert_allclose(psf, ref, rtol=0, atol=1e-9)
+    assert psf.shape == (3, len(xs), len(xs)) and abs(psf.max() - 1) < 1e-15
