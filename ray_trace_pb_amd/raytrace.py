@@ -421,8 +421,26 @@ class System:
         materials = [initial_material] + list(self.materials) + [final_material]
         if len(materials) != len(self.surfaces) + 1:
             raise ValueError("length of materials should be len(surfaces) + 1")
-        return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
-                              layout=layout)
+        custom = [s._rtpb_user_propagate() for s in self.surfaces]
+        if not any(custom):
+            return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
+                                  layout=layout)
+        # user surfaces with their own propagate: run maximal runs of built-in surfaces as fused GPU
+        # traces and hand the growing history to each user propagate in between (RT:658-659 order)
+        if not (isinstance(planes, str) and planes == "all") or layout != "aos":
+            raise ValueError("systems with user-defined propagate() support only planes='all', layout='aos'")
+        hist, i, S = rays, 0, len(self.surfaces)
+        while i < S:
+            if custom[i]:
+                hist = self.surfaces[i].propagate(hist, materials[i], materials[i + 1])
+                i += 1
+                continue
+            j = i
+            while j < S and not custom[j]:
+                j += 1
+            hist = trace_surfaces(self.surfaces[i:j], materials[i:j + 1], hist, dtype=dtype, devices=devices)
+            i = j
+        return hist
 
     # ------------------------------------------------------------------ paraxial analysis (RT:484-855)
     def _indices(self, wavelength, initial_material, final_material):
@@ -647,14 +665,24 @@ class Surface:
     _RTPB_KIND = None
     _GEOMETRY = ("propagate", "get_intersect", "get_normal", "is_pt_on_surface")
 
+    def _rtpb_kind_class(self):
+        return next((c for c in type(self).__mro__ if "_RTPB_KIND" in c.__dict__ and c._RTPB_KIND is not None), None)
+
+    def _rtpb_user_propagate(self):
+        """True for a user subclass that supplies its own ``propagate`` (the reference's plugin point,
+        RT:1092-1104, as PerfectLens does): System.ray_trace then runs that code for this surface."""
+        kind_cls = self._rtpb_kind_class()
+        base = kind_cls.propagate if kind_cls is not None else Surface.propagate
+        return type(self).propagate is not base
+
     def _rtpb_kind(self):
-        kind_cls = next((c for c in type(self).__mro__ if "_RTPB_KIND" in c.__dict__ and c._RTPB_KIND is not None),
-                        None)
+        kind_cls = self._rtpb_kind_class()
         if kind_cls is None or any(getattr(type(self), m) is not getattr(kind_cls, m) for m in self._GEOMETRY):
             raise NotImplementedError(
-                f"{type(self).__name__} overrides the surface geometry; only FlatSurface, PlaneMirror, "
-                "SphericalSurface and PerfectLens (and subclasses that do not override propagate / "
-                "get_intersect / get_normal / is_pt_on_surface) can be traced on the GPU")
+                f"{type(self).__name__} overrides the surface geometry (get_intersect / get_normal / "
+                "is_pt_on_surface) without its own propagate; the GPU kernel implements FlatSurface, "
+                "PlaneMirror, SphericalSurface and PerfectLens geometry.  Override propagate to trace a "
+                "custom surface with your own code.")
         return kind_cls._RTPB_KIND
 
     def get_normal(self, pts):

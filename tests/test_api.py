@@ -160,3 +160,24 @@ def test_material_catalogue_values():
     assert mat.Constant(1.33).n(0.5) == 1.33
     assert np.array_equal(mat.Constant(1.33).n(np.array([0.5, 0.6])), [1.33, 1.33])
     assert abs(mat.Ebaf11().n(0.5876) - 1.666) < 2e-3
+
+
+def test_user_propagate_detection():
+    class MyFlat(rt.FlatSurface):
+        def propagate(self, ray_array, material1, material2):
+            return ray_array
+
+    class Geo(rt.FlatSurface):
+        def get_intersect(self, rays, material):
+            return rays
+    assert MyFlat([0, 0, 0], [0, 0, 1], 1)._rtpb_user_propagate()
+    assert not rt.FlatSurface([0, 0, 0], [0, 0, 1], 1)._rtpb_user_propagate()
+    assert not rt.PlaneMirror([0, 0, 0], [0, 0, 1], 1)._rtpb_user_propagate()
+    assert not rt.PerfectLens(1, [0, 0, 0], [0, 0, 1], 0.5)._rtpb_user_propagate()
+    assert not Geo([0, 0, 0], [0, 0, 1], 1)._rtpb_user_propagate()
+    with pytest.raises(NotImplementedError):
+        Geo([0, 0, 0], [0, 0, 1], 1)._rtpb_kind()
+    # a system made only of user surfaces never touches the GPU
+    s = rt.System([MyFlat([0, 0, 0], [0, 0, 1], 1)], [])
+    x = np.ones((2, 8))
+    assert s.ray_trace(x, mat.Vacuum(), mat.Vacuum()) is x

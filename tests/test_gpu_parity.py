@@ -232,3 +232,30 @@ def test_timing_counters():
     C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
     lib.rtpb_timing_enable(0)
     assert cnt.value == 3 and tot.value > 0
+
+
+def test_user_surface_with_own_propagate_runs_between_gpu_segments():
+    """A Surface subclass supplying its own propagate (the reference's plugin point) is called with the
+    growing history; built-in surfaces around it run as fused GPU traces.  Here the user surface is a
+    FlatSurface whose propagate delegates to the oracle, so the whole history must equal the reference."""
+    system, m0, m1, rays, ref = build_case("c5_odt")
+
+    class OracleFlat(rt.FlatSurface):
+        calls = 0
+
+        def propagate(self, ray_array, material1, material2):
+            OracleFlat.calls += 1
+            h = np.asarray(ray_array)
+            sd = surface_to_dict(self)
+            sd["type"] = "FlatSurface"
+            return O.ray_trace([sd], [material_to_dict(material1), material_to_dict(material2)], h)
+
+    surfs = list(system.surfaces)
+    last = surfs[-1]
+    surfs[-1] = OracleFlat(last.center, last.normal, last.aperture_rad)
+    custom = rt.System(surfs, system.materials)
+    got = custom.ray_trace(rays, m0, m1)
+    assert OracleFlat.calls == 1
+    assert np.array_equal(got, ref, equal_nan=True)
+    with pytest.raises(ValueError):
+        custom.ray_trace(rays, m0, m1, planes="final")
