@@ -67,6 +67,10 @@ extern "C" {
 #define RTPB_AOS 0
 #define RTPB_SOA 1
 
+/* surface-hook interaction modes (rtpb_interact) */
+#define RTPB_REFRACT 0
+#define RTPB_REFLECT 1
+
 #define RTPB_MAX_SURFACES 63     /* history planes 0..2S must fit the 128-bit plane mask */
 #define RTPB_MAX_TABLE 4096      /* total (wavelength, n) entries over all TABLE materials */
 
@@ -156,6 +160,24 @@ int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int
                          int32_t normal_per_ray, const double* center, int32_t center_per_ray,
                          const rtpb_material* material, int32_t exclude_backward, void* rays_out, double* ts_out,
                          void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---- user Surface subclasses with their own geometry (reference plugin point RT:1071-1156) ----- */
+/* A Surface subclass that keeps RefractingSurface.propagate (RT:1160-1234) or
+   ReflectingSurface.propagate (RT:1238-1303) but supplies its own get_intersect / get_normal /
+   is_pt_on_surface.  The caller evaluates those three hooks; the library does the rest of propagate
+   on the device.  `plan` holds ONE surface (only its input_axis is read) and TWO materials (the
+   media before / after the surface); buffers are device pointers in the plan's storage type, rays
+   AOS n x 8, normals n x 3.
+   rtpb_front_side: hits_out = hits with every row NaN where rays.d . input_axis < 0 (RT:1184-1192);
+     hits_out may equal hits.
+   rtpb_interact: out = Snell refraction (mode RTPB_REFRACT, n1/n2 from the plan's materials at the
+     hit's wavelength, RT:1194-1221) or reflection (RTPB_REFLECT, RT:1266-1289) of `hits` about
+     `normals`, with position NaN where the direction is NaN (TIR) and the whole row NaN where
+     on_surface[i] == 0 (RT:1225-1226; on_surface NULL = all on). */
+int rtpb_front_side(const rtpb_plan* plan, int32_t device, const void* rays, const void* hits, int64_t n,
+                    void* hits_out, void* stream);
+int rtpb_interact(const rtpb_plan* plan, int32_t device, int32_t mode, const void* hits, const void* normals,
+                  const uint8_t* on_surface, int64_t n, void* out, void* stream);
 
 /* ---- device analysis ------------------------------------------------------------------------- */
 /* intersect_rays(ray1, ray2) (RT:164-238) on device rays (AOS, n x 8; a length-1 side broadcasts).

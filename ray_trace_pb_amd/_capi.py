@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "librtpb.so")
 RTPB_ABI_VERSION = 1
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
+RTPB_REFRACT, RTPB_REFLECT = 0, 1
 RTPB_FLAT, RTPB_SPHERE, RTPB_PLANE_MIRROR, RTPB_PERFECT_LENS = 0, 1, 2, 3
 RTPB_CONSTANT, RTPB_SELLMEIER, RTPB_POLY6, RTPB_TABLE = 0, 1, 2, 3
 RTPB_MAX_SURFACES = 63
@@ -56,6 +57,8 @@ SIGNATURES = {
     "rtpb_intersect_rays": (ctypes.c_int, [_i32, _i32, _P, _i64, _P, _i64, _P, _P]),
     "rtpb_propagate_plane": (ctypes.c_int, [_i32, _i32, _P, _i64, _P, _i32, _P, _i32, ctypes.POINTER(Material), _i32,
                                             _P, _P, _P, _i64, _P]),
+    "rtpb_front_side": (ctypes.c_int, [_P, _i32, _P, _P, _i64, _P, _P]),
+    "rtpb_interact": (ctypes.c_int, [_P, _i32, _i32, _P, _P, _P, _i64, _P, _P]),
     "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),
     "rtpb_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "rtpb_timing_enable": (ctypes.c_int, [_i32]),

@@ -515,6 +515,53 @@ __global__ __launch_bounds__(kBlock) void plane_kernel(PlaneArgs a) {
     if (a.ts) a.ts[i] = t;
 }
 
+// RefractingSurface / ReflectingSurface.propagate around a user Surface subclass's own geometry
+// hooks (RT:1160-1234, RT:1238-1303): the caller evaluates get_intersect / get_normal /
+// is_pt_on_surface; these kernels do the front-side test and the Snell / reflection step.
+struct HookArgs {
+    const void* __restrict__ rays;      // previous plane (N x 8)
+    const void* __restrict__ hits;      // get_intersect result (N x 8)
+    const void* __restrict__ normals;   // get_normal result (N x 3)
+    const uint8_t* __restrict__ on;     // is_pt_on_surface result (N), NULL = all on
+    void* __restrict__ out;
+    const DevSurface<double>* __restrict__ surf;
+    const DevMaterial<double>* __restrict__ mats;
+    const double* __restrict__ table;
+    int64_t n;
+    int32_t mode;
+};
+
+template <typename TS>
+__global__ __launch_bounds__(kBlock) void front_side_kernel(HookArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const DevSurface<double> s = load_surface<double>((cptr<DevSurface<double>>)(a.surf));
+    const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.rays), i, 0);
+    Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
+    if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < 0.0) kill(h);      // RT:1184-1192
+    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, h);
+}
+
+template <typename TS>
+__global__ __launch_bounds__(kBlock) void interact_kernel(HookArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
+    const TS* nv = static_cast<const TS*>(a.normals) + 3 * i;
+    const double Nx = nv[0], Ny = nv[1], Nz = nv[2];
+    Ray<double> o;
+    if (a.mode == RTPB_REFLECT) {
+        o = reflect<double>(h, Nx, Ny, Nz);                                      // RT:1266-1289
+    } else {
+        const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
+        const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);
+        const double n2 = material_n<double>(load_material<double>(mp + 1), h.wl, a.table);
+        o = snell<double>(h, Nx, Ny, Nz, n1, n2);                               // RT:1194-1221
+    }
+    if (a.on && !a.on[i]) kill(o);                                               // RT:1225-1226, 1293-1294
+    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, o);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------- plans
@@ -1165,6 +1212,62 @@ int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int
     else hipLaunchKernelGGL(plane_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
+}
+
+namespace {
+int hook_launch(const rtpb_plan* plan_c, int32_t device, bool interact, int32_t mode, const void* rays,
+                const void* hits, const void* normals, const uint8_t* on, int64_t n, void* out, void* stream) {
+    auto* plan = const_cast<rtpb_plan*>(plan_c);
+    if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (plan->nsurf < 1 || plan->mats.size() < 2)
+        return fail(RTPB_E_INVALID, "surface-hook plans need one surface and two materials");
+    if (mode != RTPB_REFRACT && mode != RTPB_REFLECT) return fail(RTPB_E_INVALID, "bad mode");
+    if (n < 0) return fail(RTPB_E_INVALID, "n < 0");
+    if (n == 0) return RTPB_OK;
+    if (!hits || !out || (interact ? !normals : !rays)) return fail(RTPB_E_INVALID, "NULL ray buffer");
+    if ((reinterpret_cast<uintptr_t>(hits) | reinterpret_cast<uintptr_t>(out) |
+         reinterpret_cast<uintptr_t>(interact ? nullptr : rays)) % 16)
+        return fail(RTPB_E_INVALID, "ray buffers must be 16-byte aligned");
+    DeviceGuard g(device);
+    void* blob = nullptr;
+    rc = plan_device_blob(plan, device, &blob);
+    if (rc) return rc;
+    HookArgs a{};
+    a.rays = rays;
+    a.hits = hits;
+    a.normals = normals;
+    a.on = on;
+    a.out = out;
+    a.surf = static_cast<const DevSurface<double>*>(blob);
+    a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
+    a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
+    a.n = n;
+    a.mode = mode;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+    const bool f64 = plan->dtype == RTPB_F64;
+    if (interact) {
+        if (f64) hipLaunchKernelGGL(interact_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL(interact_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
+    } else {
+        if (f64) hipLaunchKernelGGL(front_side_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL(front_side_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+}  // namespace
+
+int rtpb_front_side(const rtpb_plan* plan, int32_t device, const void* rays, const void* hits, int64_t n,
+                    void* hits_out, void* stream) {
+    return hook_launch(plan, device, false, RTPB_REFRACT, rays, hits, nullptr, nullptr, n, hits_out, stream);
+}
+
+int rtpb_interact(const rtpb_plan* plan, int32_t device, int32_t mode, const void* hits, const void* normals,
+                  const uint8_t* on_surface, int64_t n, void* out, void* stream) {
+    return hook_launch(plan, device, true, mode, nullptr, hits, normals, on_surface, n, out, stream);
 }
 
 int rtpb_set_tuning(const char* key, int64_t value) {

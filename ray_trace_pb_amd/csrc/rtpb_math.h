@@ -182,7 +182,12 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n) {
 template <typename T>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
     const T nrm = tsqrt<T>(x * x + y * y + z * z);
+#if defined(RTPB_EXP_RCP_NORMALIZE)      // experiment only: reciprocal multiply (NOT bit-exact)
+    const T inv = T(1) / nrm;
+    x = x * inv; y = y * inv; z = z * inv;
+#else
     x = x / nrm; y = y / nrm; z = z / nrm;
+#endif
     if (is_nan(x)) x = T(0);
     if (is_nan(y)) y = T(0);
     if (is_nan(z)) z = T(0);
@@ -245,6 +250,9 @@ RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz) {
 // FlatSurface / PlaneMirror .is_pt_on_surface (RT:1339-1347, RT:1405-1412)
 template <typename T>
 RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
+#if defined(RTPB_EXP_NO_ONSURFACE)       // experiment only
+    return p.x == p.x;
+#endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
     const T h = rx * s.nrm[0] + ry * s.nrm[1] + rz * s.nrm[2];
     return tabs<T>(h) < s.tol && tsqrt<T>(rx * rx + ry * ry + rz * rz) <= s.ap;
@@ -253,6 +261,9 @@ RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
 // SphericalSurface.is_pt_on_surface (RT:1518-1535): aperture about the ORIGIN-through input axis
 template <typename T>
 RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
+#if defined(RTPB_EXP_NO_ONSURFACE)       // experiment only
+    return p.x == p.x;
+#endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
     const T dist = tsqrt<T>(rx * rx + ry * ry + rz * rz);
     const bool on = tabs<T>(dist - s.absR) < s.tol;

@@ -330,6 +330,82 @@ def _resolve_devices(devices):
     return [int(d) for d in devices]
 
 
+class _AxisOnly:
+    """Lowering stand-in for a user-geometry surface: the hook kernels read only input_axis."""
+
+    def __init__(self, input_axis):
+        self.input_axis = input_axis
+        self.normal = input_axis
+        self.center = (0.0, 0.0, 0.0)
+        self.aperture_rad = np.inf
+
+    @staticmethod
+    def _rtpb_kind():
+        return C.RTPB_FLAT
+
+
+def propagate_user_geometry(surface, ray_array, material1, material2, *, devices=None):
+    """RefractingSurface.propagate (RT:1160-1234) / ReflectingSurface.propagate (RT:1238-1303) for a
+    user Surface subclass that supplies its own get_intersect / get_normal / is_pt_on_surface.
+
+    The three hooks run exactly as the user wrote them (on the history's own array type, NumPy or
+    torch); the rest of propagate -- the front-side test, the Snell / reflection step and the NaN
+    rules -- runs on the GPU (``rtpb_front_side`` / ``rtpb_interact``).  Hook order and arguments
+    follow the reference: get_intersect(last plane, material1), get_normal(unmasked hits),
+    is_pt_on_surface(front-side-masked hits)."""
+    import torch
+    on_device = _is_torch_cuda(ray_array)
+    hist = ray_array if on_device else np.asarray(ray_array)
+    if hist.ndim == 1:
+        hist = hist[None, None, :]
+    elif hist.ndim == 2:
+        hist = hist[None]
+    if hist.ndim != 3 or hist.shape[-1] != 8:
+        raise ValueError(f"rays must have shape (8,), (N, 8) or (k, N, 8); got {tuple(hist.shape)}")
+    rays = hist[-1]
+    n = rays.shape[0]
+    if on_device:
+        dev = rays.device
+    else:
+        devs = _resolve_devices(devices)
+        dev = torch.device("cuda", devs[0] if devs else torch.cuda.current_device())
+    tdt = rays.dtype if (on_device and rays.dtype == torch.float32) else torch.float64
+    code = C.RTPB_F32 if tdt == torch.float32 else C.RTPB_F64
+
+    def to_dev(a, cols):
+        t = torch.as_tensor(np.asarray(a) if not torch.is_tensor(a) else a)
+        t = t.to(device=dev, dtype=tdt).reshape(-1, cols)
+        if t.shape[0] != n:
+            t = t.expand(n, cols)
+        return t.contiguous()
+
+    hits = surface.get_intersect(rays, material1)              # user hook (RT:1181)
+    normals = surface.get_normal(hits)                          # user hook (RT:1182), on unmasked hits
+    h_d = to_dev(hits, 8)
+    n_d = to_dev(normals, 3)
+    reflect = isinstance(surface, ReflectingSurface)
+    axis = getattr(surface, "input_axis", (0.0, 0.0, 1.0))
+    low = E.lower([_AxisOnly(axis)], [material1, material2 if material2 is not None else material1],
+                  lambda: torch.unique(h_d[:, 7].double()).cpu().numpy(), code)
+    plan = E.plan_for(low)
+    lib = C.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    if not reflect:                                             # front-side test (RT:1184-1192)
+        r_d = to_dev(rays, 8)
+        C.check(lib.rtpb_front_side(plan, dev.index, r_d.data_ptr(), h_d.data_ptr(), n, h_d.data_ptr(), stream))
+    hits_user = h_d if on_device else h_d.cpu().numpy()
+    on = surface.is_pt_on_surface(hits_user)                    # user hook (RT:1225, 1293)
+    on_t = torch.as_tensor(on if torch.is_tensor(on) else np.asarray(on)).to(dev)
+    on_d = torch.broadcast_to(on_t.reshape(-1) != 0, (n,)).to(torch.uint8).contiguous()
+    out_d = torch.empty_like(h_d)
+    C.check(lib.rtpb_interact(plan, dev.index, C.RTPB_REFLECT if reflect else C.RTPB_REFRACT, h_d.data_ptr(),
+                              n_d.data_ptr(), on_d.data_ptr(), n, out_d.data_ptr(), stream))
+    new = torch.stack((h_d, out_d))
+    if on_device:
+        return torch.cat((hist.to(new.dtype), new), dim=0)
+    return np.concatenate((hist, new.cpu().numpy()), axis=0)
+
+
 class System:
     """An ordered collection of optical surfaces with the materials between them (RT:359-932).
 
@@ -421,18 +497,23 @@ class System:
         materials = [initial_material] + list(self.materials) + [final_material]
         if len(materials) != len(self.surfaces) + 1:
             raise ValueError("length of materials should be len(surfaces) + 1")
-        custom = [s._rtpb_user_propagate() for s in self.surfaces]
+        custom = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
                                   layout=layout)
-        # user surfaces with their own propagate: run maximal runs of built-in surfaces as fused GPU
-        # traces and hand the growing history to each user propagate in between (RT:658-659 order)
+        # user surfaces (own propagate, or own geometry hooks): run maximal runs of built-in surfaces
+        # as fused GPU traces and hand the growing history to each user surface in between
+        # (RT:658-659 order)
         if not (isinstance(planes, str) and planes == "all") or layout != "aos":
-            raise ValueError("systems with user-defined propagate() support only planes='all', layout='aos'")
+            raise ValueError("systems with user-defined surfaces support only planes='all', layout='aos'")
         hist, i, S = rays, 0, len(self.surfaces)
         while i < S:
             if custom[i]:
-                hist = self.surfaces[i].propagate(hist, materials[i], materials[i + 1])
+                s = self.surfaces[i]
+                if s._rtpb_user_propagate():
+                    hist = s.propagate(hist, materials[i], materials[i + 1])
+                else:
+                    hist = propagate_user_geometry(s, hist, materials[i], materials[i + 1], devices=devices)
                 i += 1
                 continue
             j = i
@@ -668,21 +749,34 @@ class Surface:
     def _rtpb_kind_class(self):
         return next((c for c in type(self).__mro__ if "_RTPB_KIND" in c.__dict__ and c._RTPB_KIND is not None), None)
 
+    @classmethod
+    def _rtpb_owner(cls, name):
+        return next(c for c in cls.__mro__ if name in c.__dict__)
+
     def _rtpb_user_propagate(self):
         """True for a user subclass that supplies its own ``propagate`` (the reference's plugin point,
         RT:1092-1104, as PerfectLens does): System.ray_trace then runs that code for this surface."""
+        return self._rtpb_owner("propagate").__module__ != __name__
+
+    def _rtpb_user_geometry(self):
+        """True for a user RefractingSurface / ReflectingSurface subclass that keeps the base propagate
+        but supplies its own get_intersect / get_normal / is_pt_on_surface (RT:1071-1156): traced by
+        propagate_user_geometry (user hooks + GPU Snell/reflection).  PerfectLens subclasses keep the
+        lens kernel: PerfectLens.propagate never calls the hooks (RT:1680-1801)."""
+        if self._rtpb_user_propagate() or not isinstance(self, (RefractingSurface, ReflectingSurface)):
+            return False
         kind_cls = self._rtpb_kind_class()
-        base = kind_cls.propagate if kind_cls is not None else Surface.propagate
-        return type(self).propagate is not base
+        if kind_cls is PerfectLens:
+            return False
+        return kind_cls is None or any(self._rtpb_owner(m).__module__ != __name__ for m in self._GEOMETRY[1:])
 
     def _rtpb_kind(self):
         kind_cls = self._rtpb_kind_class()
-        if kind_cls is None or any(getattr(type(self), m) is not getattr(kind_cls, m) for m in self._GEOMETRY):
+        if kind_cls is None or self._rtpb_user_geometry():
             raise NotImplementedError(
-                f"{type(self).__name__} overrides the surface geometry (get_intersect / get_normal / "
-                "is_pt_on_surface) without its own propagate; the GPU kernel implements FlatSurface, "
-                "PlaneMirror, SphericalSurface and PerfectLens geometry.  Override propagate to trace a "
-                "custom surface with your own code.")
+                f"{type(self).__name__} is not one of the fused-kernel surface kinds (FlatSurface, "
+                "PlaneMirror, SphericalSurface, PerfectLens); System.ray_trace / propagate trace it "
+                "through its own geometry hooks or propagate instead.")
         return kind_cls._RTPB_KIND
 
     def get_normal(self, pts):
@@ -693,7 +787,10 @@ class Surface:
 
     def propagate(self, ray_array, material1: Material, material2: Material):
         """Propagate rays through this surface alone: appends (at, after) planes to the history
-        (RT:1092-1104).  Runs the same fused GPU kernel as System.ray_trace with one surface."""
+        (RT:1092-1104).  Runs the same fused GPU kernel as System.ray_trace with one surface (user
+        geometry hooks: propagate_user_geometry)."""
+        if self._rtpb_user_geometry():
+            return propagate_user_geometry(self, ray_array, material1, material2)
         return trace_surfaces([self], [material1, material2], ray_array)
 
     def get_ray_transfer_matrix(self, n1: float, n2: float):
@@ -722,6 +819,8 @@ class ReflectingSurface(Surface):
     """Surface that reflects (RT:1237-1303); ``propagate`` runs on the GPU."""
 
     def propagate(self, ray_array, material1: Material, material2: Optional[Material] = None):
+        if self._rtpb_user_geometry():
+            return propagate_user_geometry(self, ray_array, material1, material2)
         return trace_surfaces([self], [material1, material2 if material2 is not None else material1], ray_array)
 
 

@@ -126,13 +126,16 @@ def test_lowering_descriptors():
     assert low3.key != low.key and low3.surfaces[1].on_tol == 1e-12    # float64 arithmetic for both storage types
 
 
-def test_custom_surface_geometry_is_rejected_loudly():
+def test_custom_surface_geometry_is_not_lowered_to_the_fused_kernel():
     class Wobbly(rt.FlatSurface):
         def get_normal(self, pts):
             return super().get_normal(pts) * 1.0
-    s = rt.System([Wobbly([0, 0, 0], [0, 0, 1], 1)], [])
+    # the fused kernel never runs a surface whose geometry the user replaced ...
     with pytest.raises(NotImplementedError):
-        s.ray_trace(np.zeros((1, 8)), mat.Vacuum(), mat.Vacuum())
+        E.lower([Wobbly([0, 0, 0], [0, 0, 1], 1)], [mat.Vacuum(), mat.Vacuum()], lambda: np.array([0.5]),
+                C.RTPB_F64)
+    # ... System.ray_trace routes it through propagate_user_geometry (GPU hook kernels) instead
+    assert Wobbly([0, 0, 0], [0, 0, 1], 1)._rtpb_user_geometry()
 
     class Plain(rt.SphericalSurface):     # subclass that does not touch the geometry: still lowerable
         pass
@@ -177,6 +180,27 @@ def test_user_propagate_detection():
     assert not Geo([0, 0, 0], [0, 0, 1], 1)._rtpb_user_propagate()
     with pytest.raises(NotImplementedError):
         Geo([0, 0, 0], [0, 0, 1], 1)._rtpb_kind()
+    # user geometry hooks (keep the base propagate): traced through propagate_user_geometry
+    class Bare(rt.RefractingSurface):
+        pass
+
+    class LensGeo(rt.PerfectLens):
+        def get_normal(self, pts):
+            return pts
+
+    class MirrorGeo(rt.ReflectingSurface):
+        def get_intersect(self, rays, material):
+            return rays
+    assert Geo([0, 0, 0], [0, 0, 1], 1)._rtpb_user_geometry()
+    assert Bare([0, 0, 1], [0, 0, 1], [0, 0, 0], [0, 0, 0], 1)._rtpb_user_geometry()
+    assert MirrorGeo([0, 0, 1], [0, 0, 1], [0, 0, 0], [0, 0, 0], 1)._rtpb_user_geometry()
+    assert not MirrorGeo([0, 0, 1], [0, 0, 1], [0, 0, 0], [0, 0, 0], 1)._rtpb_user_propagate()
+    assert not MyFlat([0, 0, 0], [0, 0, 1], 1)._rtpb_user_geometry()
+    assert not LensGeo(1, [0, 0, 0], [0, 0, 1], 0.5)._rtpb_user_geometry()
+    assert LensGeo(1, [0, 0, 0], [0, 0, 1], 0.5)._rtpb_kind() == C.RTPB_PERFECT_LENS
+    for s in (rt.FlatSurface([0, 0, 0], [0, 0, 1], 1), rt.PlaneMirror([0, 0, 0], [0, 0, 1], 1),
+              rt.SphericalSurface(1, [0, 0, 1], 1), rt.PerfectLens(1, [0, 0, 0], [0, 0, 1], 0.5)):
+        assert not s._rtpb_user_geometry() and not s._rtpb_user_propagate()
     # a system made only of user surfaces never touches the GPU
     s = rt.System([MyFlat([0, 0, 0], [0, 0, 1], 1)], [])
     x = np.ones((2, 8))

@@ -259,3 +259,141 @@ def test_user_surface_with_own_propagate_runs_between_gpu_segments():
     assert np.array_equal(got, ref, equal_nan=True)
     with pytest.raises(ValueError):
         custom.ray_trace(rays, m0, m1, planes="final")
+
+
+# ---------------------------------------------------------------- user geometry hooks (RT:1071-1156)
+# Surface subclasses written the way a reference user writes them: own get_intersect / get_normal /
+# is_pt_on_surface (the reference's formulas, restated here with NumPy -- or torch for device
+# histories), inheriting RefractingSurface / ReflectingSurface.propagate.
+def _xp(a):
+    return torch if torch.is_tensor(a) else np
+
+
+def _rows(pts):
+    return pts if torch.is_tensor(pts) else np.atleast_2d(pts)
+
+
+def _norm3(v):
+    return _xp(v).sqrt((v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1]) + v[..., 2] * v[..., 2])
+
+
+def _tile(vec, pts):
+    pts = _rows(pts)
+    if torch.is_tensor(pts):
+        return torch.as_tensor(vec, device=pts.device).expand(pts.shape[0], 3)
+    return np.tile(vec, (pts.shape[0], 1))
+
+
+def _on_plane(pts, center, normal, aperture):
+    pts = _rows(pts)
+    rel = pts[..., 0:3] - (torch.as_tensor(center, device=pts.device) if torch.is_tensor(pts) else center)
+    dot = (rel[..., 0] * normal[0] + rel[..., 1] * normal[1]) + rel[..., 2] * normal[2]
+    return (abs(dot) < 1e-12) & (_norm3(rel) <= aperture)
+
+
+class UserFlat(rt.RefractingSurface):
+    def __init__(self, center, normal, aperture_rad):
+        self.normal = np.asarray(normal, dtype=float)
+        super().__init__(self.normal, self.normal, center, center, aperture_rad)
+
+    def get_normal(self, pts):
+        return _tile(self.normal, pts)
+
+    def get_intersect(self, rays, material):
+        return rt.propagate_ray2plane(rays, self.normal, self.center, material, exclude_backward_propagation=True)[0]
+
+    def is_pt_on_surface(self, pts):
+        return _on_plane(pts, self.center, self.normal, self.aperture_rad)
+
+
+class UserMirror(rt.ReflectingSurface):
+    def __init__(self, center, normal, aperture_rad):
+        self.normal = np.asarray(normal, dtype=float)
+        super().__init__(self.normal, self.normal, center, center, aperture_rad)
+
+    def get_normal(self, pts):
+        return _tile(self.normal, pts)
+
+    def get_intersect(self, rays, material):
+        out, ts = rt.propagate_ray2plane(rays, self.normal, self.center, material)
+        out[ts < 0] = float("nan")
+        return out
+
+    def is_pt_on_surface(self, pts):
+        return _on_plane(pts, self.center, self.normal, self.aperture_rad)
+
+
+class UserSphere(rt.RefractingSurface):
+    def __init__(self, radius, center, aperture_rad, input_axis):
+        self.radius = radius
+        ax = np.asarray(input_axis, dtype=float)
+        super().__init__(ax, ax, center, np.asarray(center) - radius * ax, aperture_rad)
+
+    def get_normal(self, pts):
+        pts = np.atleast_2d(pts)[:, :3]
+        return (pts - self.center[None, :]) / self.radius
+
+    def get_intersect(self, rays, material):
+        rays = np.atleast_2d(rays)
+        xo, yo, zo, dx, dy, dz, ph, wl = rays.T
+        xc, yc, zc = self.center
+        B = 2 * (dx * (xo - xc) + dy * (yo - yc) + dz * (zo - zc))
+        Cq = (xo - xc) ** 2 + (yo - yc) ** 2 + (zo - zc) ** 2 - self.radius ** 2
+        with np.errstate(invalid="ignore"):
+            ts = np.stack((0.5 * (-B + np.sqrt(B ** 2 - 4 * Cq)), 0.5 * (-B - np.sqrt(B ** 2 - 4 * Cq))), axis=1)
+            ts[ts < 0] = np.inf
+        t = np.min(ts, axis=1)
+        t[t == np.inf] = np.nan
+        p0 = np.stack((xo, yo, zo), axis=1)
+        pts = p0 + np.stack((dx, dy, dz), axis=1) * t[:, None]
+        shift = np.linalg.norm(pts - p0, axis=1) * 2 * np.pi / wl * material.n(wl)
+        return np.concatenate((pts, np.stack((dx, dy, dz, ph + shift, wl), axis=1)), axis=1)
+
+    def is_pt_on_surface(self, pts):
+        pts = np.atleast_2d(pts)
+        dist = np.linalg.norm(pts[..., 0:3] - self.center, axis=-1)
+        ortho = pts[..., :3] - np.sum(pts[..., :3] * self.input_axis, axis=-1)[..., None] * self.input_axis
+        return (np.abs(dist - abs(self.radius)) < 1e-12) & (np.linalg.norm(ortho, axis=-1) <= self.aperture_rad)
+
+
+def _hooked(system, spheres=True):
+    out = []
+    for s in system.surfaces:
+        if type(s) is rt.FlatSurface:
+            out.append(UserFlat(s.center, s.normal, s.aperture_rad))
+        elif type(s) is rt.PlaneMirror:
+            out.append(UserMirror(s.center, s.normal, s.aperture_rad))
+        elif type(s) is rt.SphericalSurface and spheres:
+            out.append(UserSphere(s.radius, s.center, s.aperture_rad, s.input_axis))
+        else:
+            out.append(s)
+    return rt.System(out, system.materials)
+
+
+@pytest.mark.parametrize("name", ["stress", "c4_mirror", "c2_achromat", "tir_prism", "c1_plano_convex"])
+def test_user_geometry_hooks_bitwise_vs_reference(name):
+    """User geometry hooks + GPU front-side / Snell / reflection reproduce the reference history
+    exactly, including misses, back-facing rays, TIR, aperture clipping and user materials."""
+    system, m0, m1, rays, ref = build_case(name)
+    hooked = _hooked(system)
+    n_user = sum(s._rtpb_user_geometry() for s in hooked.surfaces)
+    assert n_user >= 1
+    got = hooked.ray_trace(rays, m0, m1)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref, equal_nan=True)
+    # one surface through Surface.propagate on its own
+    s0 = hooked.surfaces[0]
+    if s0._rtpb_user_geometry():
+        mats = [m0] + list(system.materials) + [m1]
+        one = s0.propagate(rays, mats[0], mats[1])
+        assert np.array_equal(one, ref[:3], equal_nan=True)
+
+
+def test_user_geometry_hooks_on_device_history():
+    """torch CUDA histories: the hooks receive torch tensors and the result stays on the device."""
+    system, m0, m1, rays, ref = build_case("c4_mirror")
+    hooked = _hooked(system, spheres=False)
+    assert any(s._rtpb_user_geometry() for s in hooked.surfaces)
+    got = hooked.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
+    assert got.is_cuda
+    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
