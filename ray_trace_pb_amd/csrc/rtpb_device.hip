@@ -101,6 +101,7 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
         d.ax[j] = p->ax[j];
     }
     d.R = p->R; d.R2 = p->R2; d.absR = p->absR; d.ap = p->ap; d.f = p->f; d.sin_a = p->sin_a; d.tol = p->tol;
+    d.ap_sq = p->ap_sq; d.shell_lo = p->shell_lo; d.shell_hi = p->shell_hi;
     return d;
 }
 
@@ -590,22 +591,16 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p, size_t& off_mats, size
     std::vector<unsigned char> blob(bytes, 0);
     auto* ds = reinterpret_cast<DevSurface<T>*>(blob.data());
     for (size_t k = 0; k < S; ++k) {
-        const rtpb_surface& s = p.surf[k];
-        DevSurface<T> d{};
-        d.kind = s.kind;
+        const DevSurface<double> d = lower_surface(p.surf[k]);
+        DevSurface<T>& o = ds[k];
+        o.kind = d.kind;
         for (int j = 0; j < 3; ++j) {
-            d.c[j] = T(s.center[j]);
-            d.nrm[j] = T(s.normal[j]);
-            d.ax[j] = T(s.input_axis[j]);
+            o.c[j] = T(d.c[j]);
+            o.nrm[j] = T(d.nrm[j]);
+            o.ax[j] = T(d.ax[j]);
         }
-        d.R = T(s.radius);
-        d.R2 = T(s.radius_sq);
-        d.absR = T(std::fabs(s.radius));
-        d.ap = T(s.aperture);
-        d.f = T(s.focal_len);
-        d.sin_a = T(s.sin_alpha);
-        d.tol = T(s.on_tol);
-        ds[k] = d;
+        o.R = T(d.R); o.R2 = T(d.R2); o.absR = T(d.absR); o.ap = T(d.ap); o.f = T(d.f); o.sin_a = T(d.sin_a);
+        o.tol = T(d.tol); o.ap_sq = T(d.ap_sq); o.shell_lo = T(d.shell_lo); o.shell_hi = T(d.shell_hi);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) {

@@ -12,6 +12,11 @@
 #pragma once
 
 #include <stdint.h>
+#include <string.h>
+
+#include <cmath>
+
+#include "rtpb.h"
 
 #if defined(__HIPCC__)
 #define RTPB_HD __host__ __device__ __forceinline__
@@ -41,6 +46,11 @@ struct DevSurface {
     T f;         // focal length
     T sin_a;     // sin(alpha)
     T tol;       // on-surface tolerance
+    // exact squared-distance thresholds of the on-surface tests (see lower_surface): the tests
+    // compare sums of squares with these instead of taking their square roots
+    T ap_sq;     // sqrt(s) <= ap           <=>  s <= ap_sq
+    T shell_lo;  // |sqrt(s) - |R|| < tol   <=>  shell_lo <= s <= shell_hi
+    T shell_hi;
 };
 
 template <typename T>
@@ -255,7 +265,7 @@ RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
 #endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
     const T h = rx * s.nrm[0] + ry * s.nrm[1] + rz * s.nrm[2];
-    return tabs<T>(h) < s.tol && tsqrt<T>(rx * rx + ry * ry + rz * rz) <= s.ap;
+    return tabs<T>(h) < s.tol && rx * rx + ry * ry + rz * rz <= s.ap_sq;      // norm(p - c) <= aperture
 }
 
 // SphericalSurface.is_pt_on_surface (RT:1518-1535): aperture about the ORIGIN-through input axis
@@ -265,11 +275,11 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
     return p.x == p.x;
 #endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
-    const T dist = tsqrt<T>(rx * rx + ry * ry + rz * rz);
-    const bool on = tabs<T>(dist - s.absR) < s.tol;
+    const T d2 = rx * rx + ry * ry + rz * rz;
+    const bool on = d2 >= s.shell_lo && d2 <= s.shell_hi;                      // |norm(p - c) - |R|| < tol
     const T a = p.x * s.ax[0] + p.y * s.ax[1] + p.z * s.ax[2];
     const T qx = p.x - a * s.ax[0], qy = p.y - a * s.ax[1], qz = p.z - a * s.ax[2];
-    return on && tsqrt<T>(qx * qx + qy * qy + qz * qz) <= s.ap;
+    return on && qx * qx + qy * qy + qz * qz <= s.ap_sq;                        // norm(ortho) <= aperture
 }
 
 // ------------------------------------------------------------------ one surface: (at, after)
@@ -336,6 +346,66 @@ RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T 
     const bool ok = (kind == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
     if (!ok) kill(after);
     at = ri;
+}
+
+// ------------------------------------------------------------------ host: descriptor lowering
+// Exact replacement of the on-surface square roots.  s -> RN(sqrt(s)) is monotone, so for every
+// double s >= 0 (and NaN, for which both sides are false):
+//   RN(sqrt(s)) <= ap                 <=>  s <= ap_sq            (ap_sq = largest such s)
+//   |RN(RN(sqrt(s)) - A)| < tol       <=>  shell_lo <= s <= shell_hi
+// (the second set is an interval because q -> RN(q - A) is monotone too).  The bounds are found by
+// bisection over the ordered bit patterns of non-negative doubles with the host's correctly
+// rounded sqrt, i.e. with the very predicates the reference evaluates (RT:1343-1346, RT:1528-1533).
+// Host-only (plan build / CPU harness).
+namespace host {
+inline uint64_t bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+inline double from_bits(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
+
+// largest s in [lo, hi] with pred(s), given pred(lo) and !pred(hi) and pred true..false on [lo, hi]
+template <class P> double last_true(P pred, double lo, double hi) {
+    uint64_t a = bits(lo), b = bits(hi);
+    while (b - a > 1) {
+        const uint64_t m = a + (b - a) / 2;
+        if (pred(from_bits(m))) a = m; else b = m;
+    }
+    return from_bits(a);
+}
+
+inline double sqrt_le_bound(double ap) {
+    auto P = [ap](double s) { return std::sqrt(s) <= ap; };
+    if (!P(0.0)) return -HUGE_VAL;
+    if (P(HUGE_VAL)) return HUGE_VAL;
+    return last_true(P, 0.0, HUGE_VAL);
+}
+
+inline void shell_bounds(double A, double tol, double& lo, double& hi) {
+    auto P = [A, tol](double s) { return std::fabs(std::sqrt(s) - A) < tol; };
+    const double s0 = A * A;
+    if (!(s0 >= 0.0) || !P(s0)) { lo = HUGE_VAL; hi = -HUGE_VAL; return; }       // empty
+    if (P(0.0)) lo = 0.0;
+    else lo = from_bits(bits(last_true([&](double s) { return !P(s); }, 0.0, s0)) + 1);
+    hi = P(HUGE_VAL) ? HUGE_VAL : last_true(P, s0, HUGE_VAL);
+}
+}  // namespace host
+
+inline DevSurface<double> lower_surface(const rtpb_surface& s) {
+    DevSurface<double> d{};
+    d.kind = s.kind;
+    for (int j = 0; j < 3; ++j) {
+        d.c[j] = s.center[j];
+        d.nrm[j] = s.normal[j];
+        d.ax[j] = s.input_axis[j];
+    }
+    d.R = s.radius;
+    d.R2 = s.radius_sq;
+    d.absR = std::fabs(s.radius);
+    d.ap = s.aperture;
+    d.f = s.focal_len;
+    d.sin_a = s.sin_alpha;
+    d.tol = s.on_tol;
+    d.ap_sq = host::sqrt_le_bound(s.aperture);
+    host::shell_bounds(d.absR, s.on_tol, d.shell_lo, d.shell_hi);
+    return d;
 }
 
 }  // namespace rtpb

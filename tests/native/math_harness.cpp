@@ -18,14 +18,7 @@ static int harness_trace(const rtpb_surface* surfaces, int32_t nsurf, const rtpb
                          int64_t n, TS* out) {
     using T = double;
     std::vector<DevSurface<T>> S(nsurf);
-    for (int k = 0; k < nsurf; ++k) {
-        const rtpb_surface& s = surfaces[k];
-        DevSurface<T>& d = S[k];
-        d.kind = s.kind;
-        for (int j = 0; j < 3; ++j) { d.c[j] = s.center[j]; d.nrm[j] = s.normal[j]; d.ax[j] = s.input_axis[j]; }
-        d.R = T(s.radius); d.R2 = T(s.radius_sq); d.absR = T(std::fabs(s.radius)); d.ap = T(s.aperture);
-        d.f = T(s.focal_len); d.sin_a = T(s.sin_alpha); d.tol = T(s.on_tol);
-    }
+    for (int k = 0; k < nsurf; ++k) S[k] = lower_surface(surfaces[k]);
     std::vector<DevMaterial<T>> M(nsurf + 1);
     std::vector<T> table;
     for (int k = 0; k <= nsurf; ++k) {
@@ -74,4 +67,10 @@ extern "C" int harness_trace_f64(const rtpb_surface* s, int32_t ns, const rtpb_m
 extern "C" int harness_trace_f32(const rtpb_surface* s, int32_t ns, const rtpb_material* m, const float* in,
                                  int64_t n, float* out) {
     return harness_trace<float>(s, ns, m, in, n, out);
+}
+
+// on-surface thresholds of lower_surface (rtpb_math.h): out = {ap_sq, shell_lo, shell_hi}
+extern "C" void harness_bounds(double aperture, double abs_radius, double tol, double* out) {
+    out[0] = host::sqrt_le_bound(aperture);
+    host::shell_bounds(abs_radius, tol, out[1], out[2]);
 }

@@ -28,6 +28,8 @@ def harness():
                                 "-I", os.path.join(HERE, "..", "include"), "-o", tmp, SRC], check=True)
                 os.replace(tmp, OUT)
         _lib = ctypes.CDLL(OUT)
+        _lib.harness_bounds.argtypes = [ctypes.c_double] * 3 + [ctypes.POINTER(ctypes.c_double)]
+        _lib.harness_bounds.restype = None
     return _lib
 
 

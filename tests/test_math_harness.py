@@ -1,6 +1,8 @@
 """The kernel's per-ray arithmetic (rtpb_math.h, instantiated on the host by a test-only harness)
 reproduces the reference's golden histories BIT FOR BIT, through the product's own lowering
 (ray_trace_pb_amd._engine.lower).  Runs without a GPU."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -8,7 +10,7 @@ import ray_trace_pb_amd.materials as mat
 import ray_trace_pb_amd.raytrace as rt
 from ray_trace_pb_amd import _capi as C
 from ray_trace_pb_amd import _engine as E
-from native_harness import harness_trace
+from native_harness import harness, harness_trace
 from parity import CASES, load_case
 from serialize import system_from_json
 import json
@@ -28,3 +30,52 @@ def test_kernel_math_bitwise_vs_reference(name):
     low, rays, ref = lowered_case(name)
     got = harness_trace(low, rays)
     assert np.array_equal(got, ref, equal_nan=True)
+
+
+def _up(x):
+    return np.nextafter(x, np.inf)
+
+
+def _down(x):
+    return np.nextafter(x, -np.inf)
+
+
+@pytest.mark.parametrize("ap", [25.4, 1e6, 12.7, 0.0, 1e-300, 3.0, 7.25, np.inf, -1.0, np.nan, 2.0 ** 0.5])
+def test_aperture_threshold_is_exact(ap):
+    """s <= ap_sq  <=>  sqrt(s) <= ap for every double s >= 0 (checked at and around the bound)."""
+    out = np.zeros(3)
+    harness().harness_bounds(ap, 1.0, 1e-12, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    T = out[0]
+    if np.isnan(ap) or ap < 0:
+        assert T == -np.inf
+        return
+    if np.isinf(ap):
+        assert T == np.inf
+        return
+    assert np.sqrt(T) <= ap and not np.sqrt(_up(T)) <= ap
+    for s in (ap * ap, _up(ap * ap), _down(ap * ap), T, _down(T)):
+        if s >= 0:                      # sums of squares are never negative
+            assert (np.sqrt(s) <= ap) == (s <= T)
+
+
+@pytest.mark.parametrize("A", [30.0, 25.0, 1e6, 50.0, 1e-13, 0.0, 65.8, 280.6, np.inf, 3.5e4])
+def test_sphere_shell_bounds_are_exact(A):
+    """shell_lo <= s <= shell_hi  <=>  |sqrt(s) - A| < 1e-12 (the R=1e6 quirk included: only the
+    squares whose root rounds to A itself are on the surface)."""
+    tol = 1e-12
+    out = np.zeros(3)
+    harness().harness_bounds(1.0, A, tol, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    lo, hi = out[1], out[2]
+    P = lambda s: abs(np.sqrt(s) - A) < tol  # noqa: E731
+    if np.isinf(A):
+        assert lo > hi
+        return
+    assert P(lo) and P(hi)
+    assert not P(_up(hi))
+    if lo > 0:
+        assert not P(_down(lo))
+    rng = np.random.default_rng(0)
+    for s in np.concatenate((np.linspace(lo, hi, 50), [A * A, _up(A * A), _down(A * A)],
+                             A * A * (1 + rng.normal(scale=1e-13, size=200)))):
+        if s >= 0:
+            assert P(s) == (lo <= s <= hi)
