@@ -40,7 +40,15 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 256;               // auxiliary kernels
+// The trace kernel runs one wave per workgroup: a workgroup's LDS tile and wave slot are released the
+// moment its wave finishes, so the dispatcher refills CUs wave by wave instead of waiting for the
+// slowest of four (-6 % kernel time on C2 f64 full history vs 256-thread workgroups, same occupancy).
+#if defined(RTPB_EXP_TRACE_BLOCK)          // experiment builds only (tools/ab_libs.py)
+constexpr int kTraceBlock = RTPB_EXP_TRACE_BLOCK;
+#else
+constexpr int kTraceBlock = 64;
+#endif
 constexpr int kMaxDevices = 64;
 
 thread_local std::string g_last_error;
@@ -171,7 +179,7 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
 // Only the owning wave touches its tile and LDS executes one wave's DS operations in order, so no
 // workgroup barrier is needed -- just the lgkmcnt waits (asm, with a memory clobber so the compiler
 // cannot move the tile accesses across them).
-constexpr int kWaves = kBlock / 64;
+constexpr int kWaves = kTraceBlock / 64;
 constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -279,15 +287,19 @@ __device__ __forceinline__ Ray<double> tile_load(uint4* __restrict__ tile, const
 // TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
 // global stores for the staged tiles.
 template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void trace_kernel(TraceArgs<TS> a) {
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void trace_kernel(TraceArgs<TS> a) {
     using T = double;
     constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
     constexpr bool kNT = (STORE & 2) != 0;
     __shared__ uint4 tiles[kWaves][2][kTileBytes / 16];  // two tiles per wave: "at" and "after" planes
     const int lane = threadIdx.x & 63;
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
     const int64_t ray0 = i - lane;                       // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
+#if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
+    if (blockIdx.x < RTPB_EXP_STAGGER)
+        for (unsigned k = 0; k < (blockIdx.x & 7u); ++k) __builtin_amdgcn_s_sleep(20);
+#endif
     const bool valid = i < a.n;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
     uint4* tile_b = tiles[threadIdx.x >> 6][1];
@@ -668,8 +680,9 @@ std::atomic<int> g_stage_input{0};
 
 template <typename T, int IL, int OL, int ST, int W>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
-    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, st, a);
+    const int64_t blocks = (a.n + kTraceBlock - 1) / kTraceBlock;
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kTraceBlock), 0, st,
+                       a);
     return hipGetLastError();
 }
 
