@@ -11,12 +11,11 @@ independent: no data-path collective) -> weak scaling; the step time is the max 
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line with the metric, a `roofline` object for the trace kernel (algorithmic
-bytes / kernel time from HIP events recorded around each launch on its own stream; optionally the
+bytes / average launch duration from HIP events on the launch stream around the timed launches; optionally the
 PMC-measured HBM traffic) and a `cpu_baseline` object (the NumPy port of the reference, timed on this
 host on a bounded sample, N=1 only).
 """
 import argparse
-import ctypes
 import json
 import os
 import shutil
@@ -89,6 +88,45 @@ def cpu_baseline(n_rays):
     return {"value": rate, "unit": UNIT, "cores": 1, "kind": "port",
             "sample": f"C2 system, {n_rays} rays x {reps} passes, float64 full history, 1 process "
                       f"(oracle/rt_numpy.py, reference_costs=True), {t_total:.1f} s"}
+
+
+def _cpu_worker(args):
+    """One process of the parallel CPU baseline: trace ray shard [lo, hi) repeatedly for ~`secs`."""
+    lo, hi, n_rays, secs = args
+    import ray_trace_pb_amd.materials as mat
+    import ray_trace_pb_amd.raytrace as rt
+    from oracle import rt_numpy as O
+    from serialize import material_to_dict, surface_to_dict
+    system, rays, m0, m1 = build_workload(rt, mat, n_rays, 0)
+    S = [surface_to_dict(s) for s in system.surfaces]
+    M = [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]]
+    shard = np.ascontiguousarray(rays[lo:hi])
+    O.ray_trace(S, M, shard[:64], reference_costs=True)
+    passes, t0 = 0, time.perf_counter()
+    while passes < 1 or time.perf_counter() - t0 < secs:
+        O.ray_trace(S, M, shard, reference_costs=True)
+        passes += 1
+    return passes * (hi - lo) * len(S), time.perf_counter() - t0
+
+
+def cpu_baseline_parallel(n_rays, procs, secs=4.0):
+    """SURVEY §8d mode (ii): `procs` single-threaded processes on contiguous shards of the bundle."""
+    import multiprocessing as mp
+    bounds = [(n_rays * k // procs, n_rays * (k + 1) // procs, n_rays, secs) for k in range(procs)]
+    env_old = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        # spawn (fork + exec in the child): never fork a process that has initialised the GPU
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, bounds)
+    finally:
+        if env_old is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = env_old
+    units = sum(u for u, _ in res)
+    return {"value": units / max(t for _, t in res), "unit": UNIT, "cores": procs, "kind": "port",
+            "sample": f"C2 system, {n_rays} rays split over {procs} processes, ~{secs:.0f} s each"}
 
 
 def measure_traffic(args):
@@ -168,26 +206,27 @@ def main():
         torch.cuda.synchronize()
         return
 
-    lib = C.lib()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    lib.rtpb_timing_enable(1)
+    # HIP events on the launch stream (torch's current stream, which step() launches on) bracket the K
+    # back-to-back launches: their elapsed time / K is the average launch duration.  (Per-launch event
+    # pairs would insert ~6 us of marker work between kernels -- measured by tools/launch_overhead.py.)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
         step()
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    tot_ms, launches = ctypes.c_double(), ctypes.c_int64()
-    C.check(lib.rtpb_timing_collect(ctypes.byref(tot_ms), ctypes.byref(launches)))
-    lib.rtpb_timing_enable(0)
-    kernel_ms = tot_ms.value / max(launches.value, 1)
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
@@ -214,6 +253,11 @@ def main():
         cpu = None
         if world == 1 and args.cpu_baseline == "auto":
             cpu = cpu_baseline(args.cpu_rays)
+            try:
+                procs = max(1, min(16, len(os.sched_getaffinity(0))))
+                cpu["parallel"] = cpu_baseline_parallel(args.cpu_rays, procs)
+            except Exception as e:  # noqa: BLE001 -- the single-process baseline stands on its own
+                cpu["parallel"] = {"error": repr(e)}
         line = {
             "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
@@ -226,6 +270,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (traffic / 1.0) if traffic is not None else None,
                          "kernel": "trace_kernel", "kernel_ms_avg": kernel_ms, "kernel_ms_max_rank": kernel_ms_max,
+                         "kernel_ms_method": "HIP events on the launch stream around the K launches / K",
                          "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_ray_surface": bytes_per_ray / S},
             "cpu_baseline": cpu,
         }
