@@ -350,60 +350,103 @@ __global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE
     }
 }
 
+// Device ray generators.  Every angle the reference feeds to np.cos / np.sin takes only n_thetas (or
+// n_disps) + nphis distinct values, so a first tiny kernel evaluates (cos, sin) once per distinct
+// angle -- with the same expressions, hence the same bits -- and the generator proper is pure table
+// lookups + a few multiply-adds, written through the wave's LDS tile so every store instruction
+// writes 1 KiB contiguous (like the trace kernel's planes).
+struct TrigArgs {
+    double2* __restrict__ tab;          // [n_a] (cos, sin) of the linspace angles, then [n_b] of the phis
+    int64_t n_a, n_b;
+    double start, stop, step;           // numpy.linspace(start, stop, n_a)
+    double phi_start;
+    int32_t want_a;                     // 0: the linspace values are not angles (collimated offsets)
+};
+
+__global__ __launch_bounds__(kBlock) void trig_table_kernel(TrigArgs a) {
+    const int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (j < a.n_a) {
+        if (a.want_a) {
+            // numpy.linspace: start + k*step, endpoint forced to stop (num > 1)
+            const double tt = (a.n_a > 1 && j == a.n_a - 1) ? a.stop : double(j) * a.step + a.start;
+            a.tab[j] = make_double2(cos(tt), sin(tt));
+        }
+    } else if (j < a.n_a + a.n_b) {
+        const int64_t ip = j - a.n_a;
+        const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.n_b) + a.phi_start;
+        a.tab[j] = make_double2(cos(pp), sin(pp));
+    }
+}
+
 // get_ray_fan (RT:45-96) on the device: ray k = iphi * n_thetas + itheta.
 template <typename T>
 struct FanArgs {
     T* __restrict__ out;
+    const double2* __restrict__ tab;    // trig_table_kernel output
     int64_t n_thetas, nphis;
     double pt[3], c[3], ex[3], ey[3];
-    double start, stop, step, wl;
+    double wl;
 };
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void ray_fan_kernel(FanArgs<T> a) {
-    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kTraceBlock) void ray_fan_kernel(FanArgs<T> a) {
+    __shared__ uint4 tile[kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
     const int64_t total = a.n_thetas * a.nphis;
-    if (k >= total) return;
-    const int64_t it = k % a.n_thetas, ip = k / a.n_thetas;
-    // numpy.linspace: start + k*step, endpoint forced to stop (num > 1)
-    const double tt = (a.n_thetas > 1 && it == a.n_thetas - 1) ? a.stop : double(it) * a.step + a.start;
-    const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.nphis);
-    const double ct = cos(tt), st = sin(tt), cp = cos(pp), sp = sin(pp);
-    Ray<double> r;
-    r.x = a.pt[0]; r.y = a.pt[1]; r.z = a.pt[2];
-    r.dx = a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st;
-    r.dy = a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st;
-    r.dz = a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st;
-    r.ph = 0.0;
-    r.wl = a.wl;
-    store_ray<T, RTPB_AOS>(a.out, k, 0, r);
+    const int64_t ray0 = k - lane;
+    if (ray0 >= total) return;                           // wave-uniform exit
+    if (k < total) {
+        const int64_t it = k % a.n_thetas, ip = k / a.n_thetas;
+        const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
+        const double ct = t.x, st = t.y, cp = ph.x, sp = ph.y;
+        Ray<double> r;
+        r.x = a.pt[0]; r.y = a.pt[1]; r.z = a.pt[2];
+        r.dx = a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st;
+        r.dy = a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st;
+        r.dz = a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st;
+        r.ph = 0.0;
+        r.wl = a.wl;
+        tile_write<T>(tile, lane, r);
+    }
+    lds_wait();
+    tile_flush<T, true>(tile, a.out, ray0, total, lane);
 }
 
 // get_collimated_rays (RT:99-161) on the device: ray k = idisp * nphis + iphi, position
 // pt + n1 * (off cos phi) + n2 * (off sin phi), direction = normal.
 struct CollArgs {
     void* __restrict__ out;
+    const double2* __restrict__ tab;    // trig_table_kernel output ([n_disps] unused, then nphis)
     int64_t n_disps, nphis;
     double pt[3], n1[3], n2[3], nrm[3];
-    double start, stop, step, phi_start, wl;
+    double start, stop, step, wl;
 };
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void collimated_kernel(CollArgs a) {
-    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (k >= a.n_disps * a.nphis) return;
-    const int64_t id = k / a.nphis, ip = k % a.nphis;
-    const double oo = (a.n_disps > 1 && id == a.n_disps - 1) ? a.stop : double(id) * a.step + a.start;
-    const double pp = double(ip) * 2.0 * Const<double>::pi / double(a.nphis) + a.phi_start;
-    const double oc = oo * cos(pp), os = oo * sin(pp);
-    Ray<double> r;
-    r.x = a.pt[0] + a.n1[0] * oc + a.n2[0] * os;
-    r.y = a.pt[1] + a.n1[1] * oc + a.n2[1] * os;
-    r.z = a.pt[2] + a.n1[2] * oc + a.n2[2] * os;
-    r.dx = a.nrm[0]; r.dy = a.nrm[1]; r.dz = a.nrm[2];
-    r.ph = 0.0;
-    r.wl = a.wl;
-    store_ray<T, RTPB_AOS>(static_cast<T*>(a.out), k, 0, r);
+__global__ __launch_bounds__(kTraceBlock) void collimated_kernel(CollArgs a) {
+    __shared__ uint4 tile[kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
+    const int64_t total = a.n_disps * a.nphis;
+    const int64_t ray0 = k - lane;
+    if (ray0 >= total) return;                           // wave-uniform exit
+    if (k < total) {
+        const int64_t id = k / a.nphis, ip = k % a.nphis;
+        const double oo = (a.n_disps > 1 && id == a.n_disps - 1) ? a.stop : double(id) * a.step + a.start;
+        const double2 ph = a.tab[a.n_disps + ip];
+        const double oc = oo * ph.x, os = oo * ph.y;
+        Ray<double> r;
+        r.x = a.pt[0] + a.n1[0] * oc + a.n2[0] * os;
+        r.y = a.pt[1] + a.n1[1] * oc + a.n2[1] * os;
+        r.z = a.pt[2] + a.n1[2] * oc + a.n2[2] * os;
+        r.dx = a.nrm[0]; r.dy = a.nrm[1]; r.dz = a.nrm[2];
+        r.ph = 0.0;
+        r.wl = a.wl;
+        tile_write<T>(tile, lane, r);
+    }
+    lds_wait();
+    tile_flush<T, true>(tile, static_cast<T*>(a.out), ray0, total, lane);
 }
 
 // intersect_rays (RT:164-238): closest-approach solve from the first non-singular 2x2 sub-system,
@@ -514,18 +557,25 @@ struct PlaneArgs {
 };
 
 template <typename TS>
-__global__ __launch_bounds__(kBlock) void plane_kernel(PlaneArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.in), i, 0);
-    const double* nv = a.nrm + (a.nrm_per_ray ? 3 * i : 0);
-    const double* cv = a.ctr + (a.ctr_per_ray ? 3 * i : 0);
-    DevMaterial<double> m = *a.mat;
-    const double n = material_n<double>(m, r.wl, a.table);
-    double t;
-    const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0, &t);
-    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, o);
-    if (a.ts) a.ts[i] = t;
+__global__ __launch_bounds__(kTraceBlock) void plane_kernel(PlaneArgs a) {
+    __shared__ uint4 tile[kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
+    const int64_t ray0 = i - lane;
+    if (ray0 >= a.n) return;                             // wave-uniform exit
+    if (i < a.n) {
+        const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.in), i, 0);
+        const double* nv = a.nrm + (a.nrm_per_ray ? 3 * i : 0);
+        const double* cv = a.ctr + (a.ctr_per_ray ? 3 * i : 0);
+        DevMaterial<double> m = *a.mat;
+        const double n = material_n<double>(m, r.wl, a.table);
+        double t;
+        const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0, &t);
+        tile_write<TS>(tile, lane, o);
+        if (a.ts) a.ts[i] = t;
+    }
+    lds_wait();
+    tile_flush<TS, true>(tile, static_cast<TS*>(a.out), ray0, a.n, lane);
 }
 
 // RefractingSurface / ReflectingSurface.propagate around a user Surface subclass's own geometry
@@ -545,34 +595,48 @@ struct HookArgs {
 };
 
 template <typename TS>
-__global__ __launch_bounds__(kBlock) void front_side_kernel(HookArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const DevSurface<double> s = load_surface<double>((cptr<DevSurface<double>>)(a.surf));
-    const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.rays), i, 0);
-    Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
-    if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < 0.0) kill(h);      // RT:1184-1192
-    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, h);
+__global__ __launch_bounds__(kTraceBlock) void front_side_kernel(HookArgs a) {
+    __shared__ uint4 tile[kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
+    const int64_t ray0 = i - lane;
+    if (ray0 >= a.n) return;                             // wave-uniform exit
+    if (i < a.n) {
+        const DevSurface<double> s = load_surface<double>((cptr<DevSurface<double>>)(a.surf));
+        const Ray<double> r = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.rays), i, 0);
+        Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
+        if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < 0.0) kill(h);  // RT:1184-1192
+        tile_write<TS>(tile, lane, h);
+    }
+    lds_wait();
+    tile_flush<TS, true>(tile, static_cast<TS*>(a.out), ray0, a.n, lane);   // hits_out may alias hits
 }
 
 template <typename TS>
-__global__ __launch_bounds__(kBlock) void interact_kernel(HookArgs a) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
-    const TS* nv = static_cast<const TS*>(a.normals) + 3 * i;
-    const double Nx = nv[0], Ny = nv[1], Nz = nv[2];
-    Ray<double> o;
-    if (a.mode == RTPB_REFLECT) {
-        o = reflect<double>(h, Nx, Ny, Nz);                                      // RT:1266-1289
-    } else {
-        const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
-        const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);
-        const double n2 = material_n<double>(load_material<double>(mp + 1), h.wl, a.table);
-        o = snell<double>(h, Nx, Ny, Nz, n1, n2);                               // RT:1194-1221
+__global__ __launch_bounds__(kTraceBlock) void interact_kernel(HookArgs a) {
+    __shared__ uint4 tile[kTileBytes / 16];
+    const int lane = threadIdx.x & 63;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
+    const int64_t ray0 = i - lane;
+    if (ray0 >= a.n) return;                             // wave-uniform exit
+    if (i < a.n) {
+        const Ray<double> h = load_ray<TS, RTPB_AOS>(static_cast<const TS*>(a.hits), i, 0);
+        const TS* nv = static_cast<const TS*>(a.normals) + 3 * i;
+        const double Nx = nv[0], Ny = nv[1], Nz = nv[2];
+        Ray<double> o;
+        if (a.mode == RTPB_REFLECT) {
+            o = reflect<double>(h, Nx, Ny, Nz);                                      // RT:1266-1289
+        } else {
+            const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
+            const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);
+            const double n2 = material_n<double>(load_material<double>(mp + 1), h.wl, a.table);
+            o = snell<double>(h, Nx, Ny, Nz, n1, n2);                               // RT:1194-1221
+        }
+        if (a.on && !a.on[i]) kill(o);                                               // RT:1225-1226, 1293-1294
+        tile_write<TS>(tile, lane, o);
     }
-    if (a.on && !a.on[i]) kill(o);                                               // RT:1225-1226, 1293-1294
-    store_ray<TS, RTPB_AOS>(static_cast<TS*>(a.out), i, 0, o);
+    lds_wait();
+    tile_flush<TS, true>(tile, static_cast<TS*>(a.out), ray0, a.n, lane);
 }
 
 }  // namespace
@@ -1047,6 +1111,7 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     if (n_thetas <= 0 || nphis <= 0 || !rays_out || !pt || !center_ray)
         return fail(RTPB_E_INVALID, "bad ray-fan arguments");
     if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
     const double* c = center_ray;
     // enx = cross((0,1,0), c) / |.|; eny = cross(c, enx)   (RT:79-81)
     double ex[3] = {1.0 * c[2] - 0.0 * c[1], 0.0 * c[0] - 0.0 * c[2], 0.0 * c[1] - 1.0 * c[0]};
@@ -1055,26 +1120,38 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     const double ey[3] = {c[1] * ex[2] - c[2] * ex[1], c[2] * ex[0] - c[0] * ex[2], c[0] * ex[1] - c[1] * ex[0]};
     DeviceGuard g(device);
     const int64_t total = n_thetas * nphis;
-    const unsigned blocks = static_cast<unsigned>((total + kBlock - 1) / kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    double2* tab = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tab), size_t(n_thetas + nphis) * sizeof(double2), st));
+    TrigArgs ta{};
+    ta.tab = tab;
+    ta.n_a = n_thetas;
+    ta.n_b = nphis;
+    ta.start = -theta_max;
+    ta.stop = theta_max;
+    ta.step = n_thetas > 1 ? (theta_max - (-theta_max)) / double(n_thetas - 1) : 0.0;
+    ta.phi_start = 0.0;
+    ta.want_a = 1;
+    hipLaunchKernelGGL(trig_table_kernel, dim3(static_cast<unsigned>((n_thetas + nphis + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, ta);
+    const unsigned blocks = static_cast<unsigned>((total + kTraceBlock - 1) / kTraceBlock);
     auto go = [&](auto tag) {
         using T = decltype(tag);
         FanArgs<T> a{};
         a.out = static_cast<T*>(rays_out);
+        a.tab = tab;
         a.n_thetas = n_thetas;
         a.nphis = nphis;
         for (int j = 0; j < 3; ++j) {
             a.pt[j] = pt[j]; a.c[j] = c[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
         }
-        a.start = -theta_max;
-        a.stop = theta_max;
-        a.step = n_thetas > 1 ? (theta_max - (-theta_max)) / double(n_thetas - 1) : 0.0;
         a.wl = wavelength;
-        hipLaunchKernelGGL(ray_fan_kernel<T>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+        hipLaunchKernelGGL(ray_fan_kernel<T>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     };
     if (dtype == RTPB_F64) go(double{});
-    else if (dtype == RTPB_F32) go(float{});
-    else return fail(RTPB_E_INVALID, "bad dtype");
+    else go(float{});
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(tab, st));
     return RTPB_OK;
 }
 
@@ -1110,15 +1187,25 @@ int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const do
     a.start = -displacement_max;
     a.stop = displacement_max;
     a.step = n_disps > 1 ? (displacement_max - (-displacement_max)) / double(n_disps - 1) : 0.0;
-    a.phi_start = phi_start;
     a.wl = wavelength;
     DeviceGuard g(device);
-    const unsigned blocks = static_cast<unsigned>((n_disps * nphis + kBlock - 1) / kBlock);
-    if (dtype == RTPB_F64)
-        hipLaunchKernelGGL(collimated_kernel<double>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
-    else
-        hipLaunchKernelGGL(collimated_kernel<float>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    double2* tab = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tab), size_t(n_disps + nphis) * sizeof(double2), st));
+    TrigArgs ta{};
+    ta.tab = tab;
+    ta.n_a = n_disps;
+    ta.n_b = nphis;
+    ta.phi_start = phi_start;
+    ta.want_a = 0;
+    hipLaunchKernelGGL(trig_table_kernel, dim3(static_cast<unsigned>((n_disps + nphis + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, ta);
+    a.tab = tab;
+    const unsigned blocks = static_cast<unsigned>((n_disps * nphis + kTraceBlock - 1) / kTraceBlock);
+    if (dtype == RTPB_F64) hipLaunchKernelGGL(collimated_kernel<double>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
+    else hipLaunchKernelGGL(collimated_kernel<float>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(tab, st));
     return RTPB_OK;
 }
 
@@ -1215,9 +1302,9 @@ int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int
     a.nrm_per_ray = normal_per_ray;
     a.ctr_per_ray = center_per_ray;
     a.exclude = exclude_backward;
-    const unsigned blocks = static_cast<unsigned>((n_rays + kBlock - 1) / kBlock);
-    if (dtype == RTPB_F64) hipLaunchKernelGGL(plane_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL(plane_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
+    const unsigned blocks = static_cast<unsigned>((n_rays + kTraceBlock - 1) / kTraceBlock);
+    if (dtype == RTPB_F64) hipLaunchKernelGGL(plane_kernel<double>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
+    else hipLaunchKernelGGL(plane_kernel<float>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
 }
@@ -1254,14 +1341,14 @@ int hook_launch(const rtpb_plan* plan_c, int32_t device, bool interact, int32_t 
     a.n = n;
     a.mode = mode;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+    const unsigned blocks = static_cast<unsigned>((n + kTraceBlock - 1) / kTraceBlock);
     const bool f64 = plan->dtype == RTPB_F64;
     if (interact) {
-        if (f64) hipLaunchKernelGGL(interact_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL(interact_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
+        if (f64) hipLaunchKernelGGL(interact_kernel<double>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL(interact_kernel<float>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     } else {
-        if (f64) hipLaunchKernelGGL(front_side_kernel<double>, dim3(blocks), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL(front_side_kernel<float>, dim3(blocks), dim3(kBlock), 0, st, a);
+        if (f64) hipLaunchKernelGGL(front_side_kernel<double>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
+        else hipLaunchKernelGGL(front_side_kernel<float>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     }
     HIP_TRY(hipGetLastError());
     return RTPB_OK;
