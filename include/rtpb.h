@@ -57,9 +57,13 @@ extern "C" {
 /* material kinds (Material.n overrides) */
 #define RTPB_CONSTANT 0      /* Constant  MAT:59-79:  n = c[0]                                   */
 #define RTPB_SELLMEIER 1     /* Material  MAT:39-51:  c = {b1,b2,b3,c1,c2,c3}; Vacuum = zeros    */
-#define RTPB_POLY6 2         /* Ebaf11    MAT:128-144: c = {p0..p5}, n^2 = p0+p1 w^2+p2 w^-2+...  */
-#define RTPB_TABLE 3         /* user Material subclass: n looked up by exact wavelength match in
-                                a (wavelength, n) table evaluated on the host by the subclass's n() */
+#define RTPB_POLY6 2         /* Ebaf11    MAT:128-144: c = {p0..p5}, n^2 = p0+p1 w^2+p2 w^-2+...
+                                evaluated on the device with the device pow(): within 1 ulp of the
+                                host's, but NumPy's SIMD power differs from libm pow on ~5 % of
+                                inputs, so bit-exact callers lower Ebaf11 as RTPB_TABLE instead */
+#define RTPB_TABLE 3         /* n looked up by exact wavelength match in a (wavelength, n) table
+                                evaluated on the host by the material's own n() (user subclasses;
+                                the Python front end also lowers Ebaf11 this way, see POLY6) */
 
 /* data types and layouts */
 #define RTPB_F64 0
@@ -72,7 +76,7 @@ extern "C" {
 #define RTPB_REFLECT 1
 
 #define RTPB_MAX_SURFACES 63     /* history planes 0..2S must fit the 128-bit plane mask */
-#define RTPB_MAX_TABLE 4096      /* total (wavelength, n) entries over all TABLE materials */
+#define RTPB_MAX_TABLE (1 << 22) /* total (wavelength, n) entries over all TABLE materials */
 
 /* ---- descriptors ---------------------------------------------------------------------------- */
 typedef struct rtpb_surface {
@@ -93,7 +97,8 @@ typedef struct rtpb_material {
     int32_t kind;           /* RTPB_CONSTANT ... */
     int32_t table_len;      /* RTPB_TABLE: number of (wavelength, n) pairs */
     double c[6];            /* coefficients, see kinds */
-    const double* table;    /* RTPB_TABLE: host pointer to table_len pairs {wavelength, n}; a NaN
+    const double* table;    /* RTPB_TABLE: host pointer to table_len pairs {wavelength, n}, any order
+                               (the library sorts them; lookups are binary searches); a NaN
                                wavelength key gives n(NaN).  Copied at plan creation. */
 } rtpb_material;
 
@@ -141,7 +146,9 @@ int rtpb_trace_host(const rtpb_plan* plan, const void* rays_in, int64_t n_rays, 
                     const int32_t* devices, int32_t n_devices);
 
 /* ---- device ray generators (reference RT:45-161), written straight into device memory -------- */
-/* get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray): ray k = iphi*n_thetas+itheta. */
+/* get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray): ray k = iphi*n_thetas+itheta.
+   These two evaluate cos/sin with the device libm (within 1 ulp of the host's); the *_tables variants
+   below are bit-exact against the caller's NumPy. */
 int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
                  int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength,
                  void* stream);
@@ -151,6 +158,17 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
 int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
                          int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
                          void* stream);
+
+/* Same two generators with every host-side constant supplied by the caller, so the device output is
+   bit-identical to the caller's own NumPy evaluation of RT:45-161: ex/ey (or n1/n2) basis vectors,
+   (cos, sin) pairs of the linspace thetas (2*n_thetas doubles) and of the phis (2*nphis doubles), and
+   the offsets (n_disps doubles).  Tables are HOST pointers, copied before the call returns. */
+int rtpb_ray_fan_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_thetas,
+                        int64_t nphis, const double center_ray[3], const double ex[3], const double ey[3],
+                        const double* theta_cos_sin, const double* phi_cos_sin, double wavelength, void* stream);
+int rtpb_collimated_rays_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_disps,
+                                int64_t nphis, const double normal[3], const double n1[3], const double n2[3],
+                                const double* offsets, const double* phi_cos_sin, double wavelength, void* stream);
 
 /* propagate_ray2plane(rays, normal, center, material, exclude_backward_propagation) (RT:241-306) on
    device rays (AOS n x 8).  normal / center: DEVICE pointers to 3 doubles (broadcast) or n x 3 doubles

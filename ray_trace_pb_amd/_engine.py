@@ -89,6 +89,18 @@ def lower(surfaces, materials, wavelengths, dtype):
     return low
 
 
+def distinct_wavelengths(col):
+    """Sorted distinct values of a wavelength column (NumPy or torch CUDA), NaN last -- the keys of
+    RTPB_TABLE materials.  Single-colour bundles (the common case) skip the sort."""
+    if type(col).__module__.startswith("torch"):
+        import torch
+        return np.unique(torch.unique(col.double()).cpu().numpy())
+    w = np.asarray(col, dtype=np.float64)
+    if w.size and (w == w[0]).all():
+        return w[:1].copy()
+    return np.unique(w)
+
+
 def lower_material(m, wavelengths):
     """One ``rtpb_material`` (tables keep a reference on the returned struct as ``_keep``)."""
     d = C.Material()

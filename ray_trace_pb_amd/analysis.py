@@ -2,7 +2,7 @@
 group and a chunked spot-diagram sweep that never leaves HBM (BASELINE configs[4] / C5 scale).
 
 The reference computes spot diagrams in user scripts with NumPy on the full host history; here the
-fans are generated on the GPU (``rtpb_ray_fan``), traced with only the final plane stored, and reduced
+fans are generated on the GPU (``rtpb_ray_fan_tables``), traced with only the final plane stored, and reduced
 on the GPU with a deterministic fixed-order reduction (``rtpb_spot_stats``).
 """
 import time
@@ -94,11 +94,8 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
 
 
 def _fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray, code):
-    import torch
-    d3 = C.ctypes.c_double * 3
-    C.check(C.lib().rtpb_ray_fan(buf.device.index or 0, code, buf.data_ptr(), d3(*np.asarray(pt, dtype=float).ravel()),
-                                 float(theta_max), int(n_thetas), int(nphis), d3(*np.asarray(center_ray, dtype=float)),
-                                 float(wavelength), torch.cuda.current_stream(buf.device).cuda_stream))
+    from .raytrace import fan_into
+    fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray)
 
 
 def pupil_psf(system, initial_material, final_material, source_points, wavelength, theta_max, n_thetas, nphis,

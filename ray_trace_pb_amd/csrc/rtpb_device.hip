@@ -421,6 +421,7 @@ struct CollArgs {
     int64_t n_disps, nphis;
     double pt[3], n1[3], n2[3], nrm[3];
     double start, stop, step, wl;
+    int32_t use_offsets;                // 1: offset of idisp = tab[idisp].x (the caller's np.linspace)
 };
 
 template <typename T>
@@ -433,7 +434,8 @@ __global__ __launch_bounds__(kTraceBlock) void collimated_kernel(CollArgs a) {
     if (ray0 >= total) return;                           // wave-uniform exit
     if (k < total) {
         const int64_t id = k / a.nphis, ip = k % a.nphis;
-        const double oo = (a.n_disps > 1 && id == a.n_disps - 1) ? a.stop : double(id) * a.step + a.start;
+        const double oo = a.use_offsets ? a.tab[id].x
+                          : (a.n_disps > 1 && id == a.n_disps - 1) ? a.stop : double(id) * a.step + a.start;
         const double2 ph = a.tab[a.n_disps + ip];
         const double oc = oo * ph.x, os = oo * ph.y;
         Ray<double> r;
@@ -1011,6 +1013,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
                 return fail(RTPB_E_LIMIT, "more than RTPB_MAX_TABLE wavelength table entries");
             }
             p->table.insert(p->table.end(), m.table, m.table + 2 * m.table_len);
+            sort_table(p->table.data() + p->table.size() - 2 * m.table_len, m.table_len);
         }
         m.table = nullptr;
         p->mats.push_back(m);
@@ -1104,27 +1107,68 @@ int rtpb_trace_host(const rtpb_plan* plan_c, const void* rays_in, int64_t n_rays
     return RTPB_OK;
 }
 
-int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
-                 int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength, void* stream) {
+namespace {
+// Generator tables on the device: (cos, sin) pairs [n_a] then [n_b].  With host tables (the caller's
+// own np.cos / np.sin / np.linspace values) they are copied; otherwise trig_table_kernel evaluates
+// them with the device's libm (within an ulp of the host's).
+int gen_tables(double2** tab, int64_t n_a, int64_t n_b, const double* host_a, const double* host_b, int a_pairs,
+               const TrigArgs& ta, hipStream_t st) {
+    const size_t bytes = size_t(n_a + n_b) * sizeof(double2);
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(tab), bytes, st));
+    if (host_a || host_b) {
+        // per-thread pinned staging, reused once its previous copy has completed (no stream sync)
+        thread_local struct Staging {
+            double2* buf = nullptr;
+            size_t cap = 0;
+            hipEvent_t done = nullptr;
+        } sg;
+        if (sg.done) HIP_TRY(hipEventSynchronize(sg.done));
+        if (sg.cap < bytes) {
+            if (sg.buf) HIP_TRY(hipHostFree(sg.buf));
+            sg.buf = nullptr;
+            sg.cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sg.buf), bytes, hipHostMallocDefault));
+            sg.cap = bytes;
+        }
+        if (!sg.done) HIP_TRY(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming));
+        for (int64_t j = 0; j < n_a; ++j)
+            sg.buf[j] = a_pairs ? make_double2(host_a[2 * j], host_a[2 * j + 1]) : make_double2(host_a[j], 0.0);
+        for (int64_t j = 0; j < n_b; ++j) sg.buf[n_a + j] = make_double2(host_b[2 * j], host_b[2 * j + 1]);
+        HIP_TRY(hipMemcpyAsync(*tab, sg.buf, bytes, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(sg.done, st));
+        return RTPB_OK;
+    }
+    TrigArgs a = ta;
+    a.tab = *tab;
+    hipLaunchKernelGGL(trig_table_kernel, dim3(static_cast<unsigned>((n_a + n_b + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int fan_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max, int64_t n_thetas,
+             int64_t nphis, const double c[3], const double* ex_in, const double* ey_in, const double* theta_cs,
+             const double* phi_cs, double wavelength, void* stream) {
     int rc = check_device(device);
     if (rc) return rc;
-    if (n_thetas <= 0 || nphis <= 0 || !rays_out || !pt || !center_ray)
-        return fail(RTPB_E_INVALID, "bad ray-fan arguments");
+    if (n_thetas <= 0 || nphis <= 0 || !rays_out || !pt || !c) return fail(RTPB_E_INVALID, "bad ray-fan arguments");
+    if ((theta_cs == nullptr) != (phi_cs == nullptr)) return fail(RTPB_E_INVALID, "pass both trig tables or neither");
     if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
     if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
-    const double* c = center_ray;
-    // enx = cross((0,1,0), c) / |.|; eny = cross(c, enx)   (RT:79-81)
-    double ex[3] = {1.0 * c[2] - 0.0 * c[1], 0.0 * c[0] - 0.0 * c[2], 0.0 * c[1] - 1.0 * c[0]};
-    const double en = std::sqrt(ex[0] * ex[0] + ex[1] * ex[1] + ex[2] * ex[2]);
-    for (double& v : ex) v = v / en;
-    const double ey[3] = {c[1] * ex[2] - c[2] * ex[1], c[2] * ex[0] - c[0] * ex[2], c[0] * ex[1] - c[1] * ex[0]};
+    double ex[3], ey[3];
+    if (ex_in && ey_in) {
+        for (int j = 0; j < 3; ++j) { ex[j] = ex_in[j]; ey[j] = ey_in[j]; }
+    } else {
+        // enx = cross((0,1,0), c) / |.|; eny = cross(c, enx)   (RT:79-81)
+        ex[0] = 1.0 * c[2] - 0.0 * c[1]; ex[1] = 0.0 * c[0] - 0.0 * c[2]; ex[2] = 0.0 * c[1] - 1.0 * c[0];
+        const double en = std::sqrt(ex[0] * ex[0] + ex[1] * ex[1] + ex[2] * ex[2]);
+        for (double& v : ex) v = v / en;
+        ey[0] = c[1] * ex[2] - c[2] * ex[1]; ey[1] = c[2] * ex[0] - c[0] * ex[2]; ey[2] = c[0] * ex[1] - c[1] * ex[0];
+    }
     DeviceGuard g(device);
     const int64_t total = n_thetas * nphis;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    double2* tab = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tab), size_t(n_thetas + nphis) * sizeof(double2), st));
     TrigArgs ta{};
-    ta.tab = tab;
     ta.n_a = n_thetas;
     ta.n_b = nphis;
     ta.start = -theta_max;
@@ -1132,8 +1176,9 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     ta.step = n_thetas > 1 ? (theta_max - (-theta_max)) / double(n_thetas - 1) : 0.0;
     ta.phi_start = 0.0;
     ta.want_a = 1;
-    hipLaunchKernelGGL(trig_table_kernel, dim3(static_cast<unsigned>((n_thetas + nphis + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, st, ta);
+    double2* tab = nullptr;
+    rc = gen_tables(&tab, n_thetas, nphis, theta_cs, phi_cs, 1, ta, st);
+    if (rc) return rc;
     const unsigned blocks = static_cast<unsigned>((total + kTraceBlock - 1) / kTraceBlock);
     auto go = [&](auto tag) {
         using T = decltype(tag);
@@ -1155,51 +1200,57 @@ int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[
     return RTPB_OK;
 }
 
-int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
-                         int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
-                         void* stream) {
+int collimated_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
+                    int64_t n_disps, int64_t nphis, double phi_start, const double nv[3], const double* n1_in,
+                    const double* n2_in, const double* offsets, const double* phi_cs, double wavelength,
+                    void* stream) {
     int rc = check_device(device);
     if (rc) return rc;
-    if (n_disps <= 0 || nphis <= 0 || !rays_out || !pt || !normal)
+    if (n_disps <= 0 || nphis <= 0 || !rays_out || !pt || !nv)
         return fail(RTPB_E_INVALID, "bad collimated-ray arguments");
+    if ((offsets == nullptr) != (phi_cs == nullptr)) return fail(RTPB_E_INVALID, "pass both tables or neither");
     if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
     if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
     CollArgs a{};
     a.out = rays_out;
     a.n_disps = n_disps;
     a.nphis = nphis;
-    const double* nv = normal;
-    // n1 = (0,1,0) x normal, or normal x (1,0,0) when that vanishes; n2 = normal x n1 (RT:135-144)
-    double n1[3] = {1.0 * nv[2] - 0.0 * nv[1], 0.0 * nv[0] - 0.0 * nv[2], 0.0 * nv[1] - 1.0 * nv[0]};
-    if (std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]) == 0.0) {
-        n1[0] = nv[1] * 0.0 - nv[2] * 0.0;
-        n1[1] = nv[2] * 1.0 - nv[0] * 0.0;
-        n1[2] = nv[0] * 0.0 - nv[1] * 1.0;
+    double n1[3], n2[3];
+    if (n1_in && n2_in) {
+        for (int j = 0; j < 3; ++j) { n1[j] = n1_in[j]; n2[j] = n2_in[j]; }
+    } else {
+        // n1 = (0,1,0) x normal, or normal x (1,0,0) when that vanishes; n2 = normal x n1 (RT:135-144)
+        n1[0] = 1.0 * nv[2] - 0.0 * nv[1]; n1[1] = 0.0 * nv[0] - 0.0 * nv[2]; n1[2] = 0.0 * nv[1] - 1.0 * nv[0];
+        if (std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]) == 0.0) {
+            n1[0] = nv[1] * 0.0 - nv[2] * 0.0;
+            n1[1] = nv[2] * 1.0 - nv[0] * 0.0;
+            n1[2] = nv[0] * 0.0 - nv[1] * 1.0;
+        }
+        const double l1 = std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]);
+        for (double& v : n1) v = v / l1;
+        n2[0] = nv[1] * n1[2] - nv[2] * n1[1]; n2[1] = nv[2] * n1[0] - nv[0] * n1[2];
+        n2[2] = nv[0] * n1[1] - nv[1] * n1[0];
+        const double l2 = std::sqrt(n2[0] * n2[0] + n2[1] * n2[1] + n2[2] * n2[2]);
+        for (double& v : n2) v = v / l2;
     }
-    const double l1 = std::sqrt(n1[0] * n1[0] + n1[1] * n1[1] + n1[2] * n1[2]);
-    for (double& v : n1) v = v / l1;
-    double n2[3] = {nv[1] * n1[2] - nv[2] * n1[1], nv[2] * n1[0] - nv[0] * n1[2], nv[0] * n1[1] - nv[1] * n1[0]};
-    const double l2 = std::sqrt(n2[0] * n2[0] + n2[1] * n2[1] + n2[2] * n2[2]);
-    for (double& v : n2) v = v / l2;
     for (int j = 0; j < 3; ++j) {
         a.pt[j] = pt[j]; a.n1[j] = n1[j]; a.n2[j] = n2[j]; a.nrm[j] = nv[j];
     }
     a.start = -displacement_max;
     a.stop = displacement_max;
     a.step = n_disps > 1 ? (displacement_max - (-displacement_max)) / double(n_disps - 1) : 0.0;
+    a.use_offsets = offsets != nullptr;
     a.wl = wavelength;
     DeviceGuard g(device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    double2* tab = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tab), size_t(n_disps + nphis) * sizeof(double2), st));
     TrigArgs ta{};
-    ta.tab = tab;
     ta.n_a = n_disps;
     ta.n_b = nphis;
     ta.phi_start = phi_start;
     ta.want_a = 0;
-    hipLaunchKernelGGL(trig_table_kernel, dim3(static_cast<unsigned>((n_disps + nphis + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, st, ta);
+    double2* tab = nullptr;
+    rc = gen_tables(&tab, n_disps, nphis, offsets, phi_cs, 0, ta, st);
+    if (rc) return rc;
     a.tab = tab;
     const unsigned blocks = static_cast<unsigned>((n_disps * nphis + kTraceBlock - 1) / kTraceBlock);
     if (dtype == RTPB_F64) hipLaunchKernelGGL(collimated_kernel<double>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
@@ -1207,6 +1258,36 @@ int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const do
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFreeAsync(tab, st));
     return RTPB_OK;
+}
+}  // namespace
+
+int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
+                 int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength, void* stream) {
+    return fan_impl(device, dtype, rays_out, pt, theta_max, n_thetas, nphis, center_ray, nullptr, nullptr, nullptr,
+                    nullptr, wavelength, stream);
+}
+
+int rtpb_ray_fan_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_thetas,
+                        int64_t nphis, const double center_ray[3], const double ex[3], const double ey[3],
+                        const double* theta_cos_sin, const double* phi_cos_sin, double wavelength, void* stream) {
+    if (!ex || !ey || !theta_cos_sin || !phi_cos_sin) return fail(RTPB_E_INVALID, "NULL table argument");
+    return fan_impl(device, dtype, rays_out, pt, 0.0, n_thetas, nphis, center_ray, ex, ey, theta_cos_sin, phi_cos_sin,
+                    wavelength, stream);
+}
+
+int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
+                         int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
+                         void* stream) {
+    return collimated_impl(device, dtype, rays_out, pt, displacement_max, n_disps, nphis, phi_start, normal, nullptr,
+                           nullptr, nullptr, nullptr, wavelength, stream);
+}
+
+int rtpb_collimated_rays_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_disps,
+                                int64_t nphis, const double normal[3], const double n1[3], const double n2[3],
+                                const double* offsets, const double* phi_cos_sin, double wavelength, void* stream) {
+    if (!n1 || !n2 || !offsets || !phi_cos_sin) return fail(RTPB_E_INVALID, "NULL table argument");
+    return collimated_impl(device, dtype, rays_out, pt, 0.0, n_disps, nphis, 0.0, normal, n1, n2, offsets, phi_cos_sin,
+                           wavelength, stream);
 }
 
 int rtpb_intersect_rays(int32_t device, int32_t dtype, const void* ray1, int64_t n1, const void* ray2, int64_t n2,
@@ -1285,7 +1366,11 @@ int rtpb_propagate_plane(int32_t device, int32_t dtype, const void* rays_in, int
     dm.table_off = 0;
     dm.table_len = static_cast<int32_t>(ntab);
     std::memcpy(host.data(), &dm, sizeof(dm));
-    if (ntab) std::memcpy(host.data() + align256(sizeof(dm)), material->table, size_t(2 * ntab) * sizeof(double));
+    if (ntab) {
+        double* t = reinterpret_cast<double*>(host.data() + align256(sizeof(dm)));
+        std::memcpy(t, material->table, size_t(2 * ntab) * sizeof(double));
+        sort_table(t, ntab);
+    }
     DeviceGuard g(device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     HIP_TRY(hipMemcpyAsync(workspace, host.data(), need, hipMemcpyHostToDevice, st));

@@ -14,6 +14,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "rtpb.h"
@@ -129,14 +130,21 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
                      m.c[4] * tpow<T>(wl, T(-6)) + m.c[5] * tpow<T>(wl, T(-8));
         return tsqrt<T>(n2);
     }
-    default: {                                                       // TABLE: user Material.n
-        const bool want_nan = is_nan(wl);
-        T out = qnan<T>();
-        for (int k = 0; k < m.table_len; ++k) {
-            const T key = table[2 * (m.table_off + k)];
-            if (want_nan ? is_nan(key) : key == wl) { out = table[2 * (m.table_off + k) + 1]; break; }
+    default: {                                                       // TABLE: host-evaluated n(lambda)
+        // (wavelength, n) pairs sorted by wavelength, NaN keys last (sort_table): binary search for
+        // the exact wavelength; NaN compares false, so NaN keys behave as +inf in the search.
+        const int len = m.table_len, off = m.table_off;
+        if (is_nan(wl)) {
+            const bool has = len > 0 && is_nan(T(table[2 * (off + len - 1)]));
+            return has ? T(table[2 * (off + len - 1) + 1]) : qnan<T>();
         }
-        return out;
+        int lo = 0, hi = len;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (T(table[2 * (off + mid)]) < wl) lo = mid + 1;
+            else hi = mid;
+        }
+        return (lo < len && T(table[2 * (off + lo)]) == wl) ? T(table[2 * (off + lo) + 1]) : qnan<T>();
     }
     }
 }
@@ -387,6 +395,17 @@ inline void shell_bounds(double A, double tol, double& lo, double& hi) {
     hi = P(HUGE_VAL) ? HUGE_VAL : last_true(P, s0, HUGE_VAL);
 }
 }  // namespace host
+
+// Order (wavelength, n) pairs by wavelength with NaN keys last, as material_n's search expects.
+inline void sort_table(double* pairs, int64_t n) {
+    struct P { double k, v; };
+    P* p = reinterpret_cast<P*>(pairs);
+    std::sort(p, p + n, [](const P& a, const P& b) {
+        const bool an = a.k != a.k, bn = b.k != b.k;
+        if (an || bn) return !an && bn;
+        return a.k < b.k;
+    });
+}
 
 inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     DevSurface<double> d{};

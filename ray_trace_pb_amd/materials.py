@@ -8,10 +8,12 @@ descriptor each material lowers to (:meth:`Material._rtpb_lower`):
 
 * Sellmeier ``Material`` (incl. ``Vacuum`` and the glass catalogue)  -> RTPB_SELLMEIER  (MAT:39-51)
 * ``Constant``                                                          -> RTPB_CONSTANT   (MAT:59-79)
-* ``Ebaf11`` (6-term polynomial in lambda^2, lambda^-2k)               -> RTPB_POLY6      (MAT:128-144)
-* any user subclass that overrides ``n`` (the reference's documented plugin point, MAT:39-44)
-  -> RTPB_TABLE: ``n`` is evaluated on the host at the distinct wavelengths of the ray bundle and
-  the kernel looks each ray's value up, so arbitrary user dispersion laws trace on the GPU unchanged.
+* ``Ebaf11`` (6-term polynomial in lambda^2, lambda^-2k, MAT:128-144) and any user subclass that
+  overrides ``n`` (the reference's documented plugin point, MAT:39-44) -> RTPB_TABLE: ``n`` is
+  evaluated on the host, by the material's own NumPy code, at the distinct wavelengths of the ray
+  bundle and the kernel looks each ray's value up (binary search), so arbitrary dispersion laws trace
+  on the GPU with the reference's exact values.  (Ebaf11 is not sent as RTPB_POLY6: NumPy's SIMD
+  ``power`` and the device ``pow`` disagree in the last bit on ~5 % of wavelengths.)
 """
 import numpy as np
 
@@ -115,8 +117,9 @@ class Ebaf11(Material):
         return np.sqrt(n_sqr)
 
     def _rtpb_lower(self):
-        if type(self).n is Ebaf11.n:
-            return RTPB_POLY6, tuple(self.params)
+        # Lowered as a host-evaluated (wavelength, n) table, not RTPB_POLY6: NumPy evaluates
+        # wavelength**-2k with its SIMD power, which differs from libm/device pow() in the last bit
+        # on ~5 % of wavelengths (AVX-512 hosts), and bit-exactness needs the reference's own n().
         return None
 
 

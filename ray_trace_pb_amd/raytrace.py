@@ -20,6 +20,7 @@ What runs where
   host-side NumPy/Matplotlib, as in the reference (they are O(S) or set-up work, SURVEY.md §2 rows
   7-9, 11-12).
 """
+import functools
 from collections.abc import Sequence
 from copy import deepcopy
 from typing import Optional
@@ -52,7 +53,7 @@ def get_ray_fan(pt, theta_max: float, n_thetas: int, wavelengths, nphis: int = 1
     cos(theta) c + cos(phi) sin(theta) ex + sin(phi) sin(theta) ey with ex = y x c / |.|, ey = c x ex,
     theta in linspace(-theta_max, theta_max, n_thetas), phi = k 2 pi / nphis.  Phase 0.
 
-    With ``device`` (a torch CUDA device), the fan is generated directly in HBM by the ``rtpb_ray_fan``
+    With ``device`` (a torch CUDA device), the fan is generated directly in HBM by the ``rtpb_ray_fan_tables``
     kernel and returned as a torch tensor (``wavelengths`` must then be a scalar)."""
     center_ray = np.array(center_ray)
     if np.linalg.norm(center_ray) != 1:
@@ -80,13 +81,45 @@ def _ray_fan_device(pt, theta_max, n_thetas, wavelength, nphis, center_ray, devi
     dev = torch.device(device)
     tdt = torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64
     out = torch.empty((n_thetas * nphis, 8), dtype=tdt, device=dev)
-    d3 = C.ctypes.c_double * 3
-    pt3 = d3(*np.asarray(pt, dtype=float).ravel())
-    c3 = d3(*center_ray.astype(float))
-    C.check(C.lib().rtpb_ray_fan(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
-                                 out.data_ptr(), pt3, float(theta_max), int(n_thetas), int(nphis), c3,
-                                 float(wavelength), torch.cuda.current_stream(dev).cuda_stream))
+    fan_into(out, pt, theta_max, n_thetas, wavelength, nphis, center_ray)
     return out
+
+
+@functools.lru_cache(maxsize=16)
+def _fan_tables(theta_max, n_thetas, nphis, center_ray, center_dtype):
+    """Host-side values of RT:71-81 (cached: a sweep reuses one fan shape for every field point)."""
+    center_ray = np.array(center_ray, dtype=center_dtype)
+    thetas = np.linspace(-theta_max, theta_max, n_thetas)
+    phis = np.arange(nphis) * 2 * np.pi / nphis
+    enx = np.cross(np.array([0, 1, 0]), center_ray)
+    enx = enx / np.linalg.norm(enx)
+    eny = np.cross(center_ray, enx)
+    tcs = np.ascontiguousarray(np.stack((np.cos(thetas), np.sin(thetas)), axis=1), dtype=np.float64)
+    pcs = np.ascontiguousarray(np.stack((np.cos(phis), np.sin(phis)), axis=1), dtype=np.float64)
+    for a in (enx, eny, tcs, pcs):
+        a.setflags(write=False)
+    return enx, eny, tcs, pcs
+
+
+def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0, 1)):
+    """Write get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray) into the torch CUDA
+    buffer ``buf`` ((n_thetas*nphis, 8), float64 or float32) on its current stream.
+
+    Every host-side value of RT:71-81 -- the linspace thetas, the phis, their np.cos / np.sin, and the
+    enx / eny basis -- is evaluated here with NumPy exactly as the reference does (n_thetas + nphis
+    trig evaluations instead of n_thetas * nphis); the kernel does the per-ray products in the
+    reference's order, so the device fan is bit-identical to the reference's."""
+    import torch
+    center_ray = np.array(center_ray)
+    enx, eny, tcs, pcs = _fan_tables(float(theta_max), int(n_thetas), int(nphis), tuple(center_ray.tolist()),
+                                     center_ray.dtype.str)
+    vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (pt, center_ray, enx, eny)]
+    code = C.RTPB_F64 if buf.dtype == torch.float64 else C.RTPB_F32
+    C.check(C.lib().rtpb_ray_fan_tables(buf.device.index or 0, code, buf.data_ptr(), vec[0].ctypes.data,
+                                        int(n_thetas), int(nphis), vec[1].ctypes.data, vec[2].ctypes.data,
+                                        vec[3].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, float(wavelength),
+                                        torch.cuda.current_stream(buf.device).cuda_stream))
+    return buf
 
 
 def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: int = 1, phi_start: float = 0.,
@@ -95,21 +128,12 @@ def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: 
 
     index = idisp*nphis + iphi; position pt + off (n1 cos phi + n2 sin phi) with n1 = y x normal
     (or normal x x when normal is along y), n2 = normal x n1; offsets linspace(-dmax, dmax, n_disps).
-    With ``device`` the bundle is generated in HBM by ``rtpb_collimated_rays`` (scalar wavelength)."""
+    With ``device`` the bundle is generated in HBM by ``rtpb_collimated_rays_tables`` (scalar wavelength)."""
     if np.abs(np.linalg.norm(normal) - 1) > 1e-12:
         raise ValueError("normal must be a normalized vector")
     if device is not None:
-        import torch
-        dev = torch.device(device)
-        tdt = torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64
-        out = torch.empty((n_disps * nphis, 8), dtype=tdt, device=dev)
-        d3 = C.ctypes.c_double * 3
-        C.check(C.lib().rtpb_collimated_rays(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
-                                             out.data_ptr(), d3(*np.asarray(pt, dtype=float).ravel()),
-                                             float(displacement_max), int(n_disps), int(nphis), float(phi_start),
-                                             d3(*np.asarray(normal, dtype=float).ravel()), float(wavelengths),
-                                             torch.cuda.current_stream(dev).cuda_stream))
-        return out
+        return _collimated_device(pt, displacement_max, n_disps, wavelengths, nphis, phi_start, normal, device,
+                                  dtype)
     phis = np.arange(nphis) * 2 * np.pi / nphis + phi_start
     offs = np.linspace(-displacement_max, displacement_max, n_disps)
     pp, oo = np.meshgrid(phis, offs)
@@ -127,6 +151,33 @@ def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: 
     rays[:, 3:6] = normal
     rays[:, 7] = wavelengths
     return rays
+
+
+def _collimated_device(pt, displacement_max, n_disps, wavelength, nphis, phi_start, normal, device, dtype):
+    """get_collimated_rays in HBM: the host-side values of RT:128-144 (phis, offsets, their cos/sin,
+    the n1/n2 basis) come from NumPy exactly as in the reference, the per-ray products from
+    ``rtpb_collimated_rays_tables`` -- bit-identical to the reference's rays."""
+    import torch
+    dev = torch.device(device)
+    tdt = torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64
+    out = torch.empty((n_disps * nphis, 8), dtype=tdt, device=dev)
+    phis = np.arange(nphis) * 2 * np.pi / nphis + phi_start
+    offs = np.ascontiguousarray(np.linspace(-displacement_max, displacement_max, n_disps), dtype=np.float64)
+    normal = np.array(normal).squeeze()
+    n1 = np.cross(np.array([0, 1, 0]), normal)
+    if np.linalg.norm(n1) == 0:
+        n1 = np.cross(normal, np.array([1, 0, 0]))
+    n1 = n1 / np.linalg.norm(n1)
+    n2 = np.cross(normal, n1)
+    n2 = n2 / np.linalg.norm(n2)
+    pcs = np.ascontiguousarray(np.stack((np.cos(phis), np.sin(phis)), axis=1), dtype=np.float64)
+    vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (pt, normal, n1, n2)]
+    C.check(C.lib().rtpb_collimated_rays_tables(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
+                                                out.data_ptr(), vec[0].ctypes.data, int(n_disps), int(nphis),
+                                                vec[1].ctypes.data, vec[2].ctypes.data, vec[3].ctypes.data,
+                                                offs.ctypes.data, pcs.ctypes.data, float(wavelength),
+                                                torch.cuda.current_stream(dev).cuda_stream))
+    return out
 
 
 # =============================================================================== ray utilities
@@ -219,7 +270,7 @@ def propagate_ray2plane(rays, normal, center, material: Material, exclude_backwa
 
     nv, n_per = plane_vec(normal)
     cv, c_per = plane_vec(center)
-    low = E.lower_material(material, lambda: torch.unique(r[:, 7]).cpu().numpy())
+    low = E.lower_material(material, lambda: E.distinct_wavelengths(r[:, 7]))
     ws = torch.empty(256 + 16 * max(low.table_len, 1), dtype=torch.uint8, device=dev)
     out = torch.empty_like(r)
     ts = torch.empty(n, dtype=torch.float64, device=dev)
@@ -292,10 +343,7 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     last = rays[-1]
 
     def wavelengths():
-        if on_device:
-            import torch
-            return torch.unique(last[:, 7].double()).cpu().numpy()
-        return np.unique(np.asarray(last[:, 7], dtype=np.float64))
+        return E.distinct_wavelengths(last[:, 7])
 
     low = E.lower(surfaces, materials, wavelengths, code)
     layout_code = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
@@ -386,7 +434,7 @@ def propagate_user_geometry(surface, ray_array, material1, material2, *, devices
     reflect = isinstance(surface, ReflectingSurface)
     axis = getattr(surface, "input_axis", (0.0, 0.0, 1.0))
     low = E.lower([_AxisOnly(axis)], [material1, material2 if material2 is not None else material1],
-                  lambda: torch.unique(h_d[:, 7].double()).cpu().numpy(), code)
+                  lambda: E.distinct_wavelengths(h_d[:, 7]), code)
     plan = E.plan_for(low)
     lib = C.lib()
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -30,8 +30,10 @@ static int harness_trace(const rtpb_surface* surfaces, int32_t nsurf, const rtpb
         if (zero) d.kind = VACUUM;
         d.table_off = static_cast<int32_t>(table.size() / 2);
         d.table_len = m.kind == RTPB_TABLE ? m.table_len : 0;
-        if (m.kind == RTPB_TABLE)
+        if (m.kind == RTPB_TABLE) {
             for (int j = 0; j < 2 * m.table_len; ++j) table.push_back(T(m.table[j]));
+            sort_table(table.data() + table.size() - 2 * m.table_len, m.table_len);
+        }
     }
     const int64_t P = 2 * nsurf + 1;
     for (int64_t i = 0; i < n; ++i) {

@@ -113,12 +113,13 @@ def test_lowering_descriptors():
     assert low.surfaces[6].sin_alpha == np.sin(lens.alpha) and low.surfaces[6].focal_len == lens.focal_len
     mk = [low.materials[k].kind for k in range(low.nsurf + 1)]
     assert mk == [C.RTPB_SELLMEIER, C.RTPB_SELLMEIER, C.RTPB_SELLMEIER, C.RTPB_SELLMEIER, C.RTPB_CONSTANT,
-                  C.RTPB_POLY6, C.RTPB_SELLMEIER, C.RTPB_SELLMEIER, C.RTPB_TABLE, C.RTPB_SELLMEIER,
+                  C.RTPB_TABLE, C.RTPB_SELLMEIER, C.RTPB_SELLMEIER, C.RTPB_TABLE, C.RTPB_SELLMEIER,
                   C.RTPB_SELLMEIER, C.RTPB_SELLMEIER]
-    tab = low.tables[0].reshape(-1, 2)
     uniq = np.unique(rays[:, 7])
-    assert np.array_equal(tab[:, 0], uniq, equal_nan=True) and np.isnan(tab[-1, 0])
-    assert np.array_equal(tab[:, 1], mats[8].n(uniq), equal_nan=True)
+    for tab, m in zip(low.tables, (mats[5], mats[8])):      # Ebaf11 (host NumPy power) and the user Cauchy
+        tab = tab.reshape(-1, 2)
+        assert np.array_equal(tab[:, 0], uniq, equal_nan=True) and np.isnan(tab[-1, 0])
+        assert np.array_equal(tab[:, 1], m.n(uniq), equal_nan=True)
     # same content -> same plan-cache key; different dtype -> different key
     low2 = E.lower(system.surfaces, mats, lambda: np.unique(rays[:, 7]), C.RTPB_F64)
     assert low.key == low2.key
