@@ -25,4 +25,8 @@ step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $
 step pmc_all 900 bash tools/pmc_profile.sh $P/pmc_all --planes all
 step pmc_final 900 bash tools/pmc_profile.sh $P/pmc_final --planes final
 step sweep 600 python tools/perf_sweep.py --configs c2,c5,c4
+step bench_aux 300 python tools/bench_aux.py
+step rocprof_aux 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof_aux -o aux -- python3 tools/bench_aux.py
+step configs_c3_c4_full 900 python tools/configs_full.py
+step c5_sweep_full 900 python tools/c5_sweep.py
 exit 0
