@@ -179,7 +179,6 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
 // Only the owning wave touches its tile and LDS executes one wave's DS operations in order, so no
 // workgroup barrier is needed -- just the lgkmcnt waits (asm, with a memory clobber so the compiler
 // cannot move the tile accesses across them).
-constexpr int kWaves = kTraceBlock / 64;
 constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -286,14 +285,23 @@ __device__ __forceinline__ Ray<double> tile_load(uint4* __restrict__ tile, const
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic,
 // TS storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal
 // global stores for the staged tiles.
+// Workgroup size per variant: the LDS-staged AoS kernels run one wave per workgroup (see kTraceBlock);
+// the direct-store variants (SoA output, unstaged AoS) keep four-wave workgroups, which measured faster
+// for their strided stores (C5 SoA: 0.53 vs 0.69 ms).
+constexpr int trace_block(int out_layout, int store) {
+    return (out_layout == RTPB_AOS && (store & 1)) ? kTraceBlock : 256;
+}
+
 template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE>
-__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void trace_kernel(TraceArgs<TS> a) {
+__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+void trace_kernel(TraceArgs<TS> a) {
+    constexpr int kB = trace_block(OUT_LAYOUT, STORE);
     using T = double;
     constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
     constexpr bool kNT = (STORE & 2) != 0;
-    __shared__ uint4 tiles[kWaves][2][kTileBytes / 16];  // two tiles per wave: "at" and "after" planes
+    __shared__ uint4 tiles[kB / 64][2][kTileBytes / 16];  // two tiles per wave: "at" and "after" planes
     const int lane = threadIdx.x & 63;
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kTraceBlock + threadIdx.x;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
     const int64_t ray0 = i - lane;                       // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
 #if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
@@ -746,9 +754,9 @@ std::atomic<int> g_stage_input{0};
 
 template <typename T, int IL, int OL, int ST, int W>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
-    const int64_t blocks = (a.n + kTraceBlock - 1) / kTraceBlock;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kTraceBlock), 0, st,
-                       a);
+    constexpr int kB = trace_block(OL, ST);
+    const int64_t blocks = (a.n + kB - 1) / kB;
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kB), 0, st, a);
     return hipGetLastError();
 }
 

@@ -427,3 +427,26 @@ def test_material_dispersion_bitwise_over_wavelength_sweep(material):
     got = system.ray_trace(rays, mat.Vacuum(), mat.Vacuum())
     ref = oracle(system, mat.Vacuum(), mat.Vacuum(), rays)
     assert np.array_equal(got, ref, equal_nan=True)
+
+
+def test_more_than_2_31_rays_in_one_launch():
+    """Maximum sizes: one trace of 2^31 + 4633 rays (int64 ray indexing, > 2^25 workgroups), float32
+    storage, final plane only (68.7 GB in + 68.7 GB out of HBM).  Rays on both sides of index 2^31 and
+    at the very end are bit-exact against the oracle on the same float32 input."""
+    system, m0, m1, _, _ = build_case("c1_plano_convex")
+    nt = nph = 46341                                  # 46341^2 = 2^31 + 4633
+    n = nt * nph
+    assert n > 2 ** 31
+    rays = torch.empty((n, 8), dtype=torch.float32, device=DEV)
+    rt.fan_into(rays, [0.0, 0.0, -5.0], 0.2, nt, 0.5, nph)
+    out = system.ray_trace(rays, m0, m1, planes="final", dtype="float32")
+    assert out.shape == (1, n, 8)
+    picks = np.r_[0:64, 2 ** 31 - 2048:2 ** 31 + 2048, n - 2048:n]
+    idx = torch.from_numpy(picks).to(DEV)
+    r_in = rays.index_select(0, idx).double().cpu().numpy()
+    got = out[0].index_select(0, idx).cpu().numpy()
+    del rays, out
+    torch.cuda.empty_cache()
+    ref = oracle(system, m0, m1, r_in)[-1].astype(np.float32)
+    assert np.array_equal(got, ref, equal_nan=True)
+    assert np.isfinite(got[:, 0]).sum() > 1000        # not an all-NaN comparison
