@@ -87,7 +87,19 @@ def cpu_baseline(n_rays):
     rate = reps * n_rays * len(S) / t_total
     return {"value": rate, "unit": UNIT, "cores": 1, "kind": "port",
             "sample": f"C2 system, {n_rays} rays x {reps} passes, float64 full history, 1 process "
-                      f"(oracle/rt_numpy.py, reference_costs=True), {t_total:.1f} s"}
+                      f"(oracle/rt_numpy.py, reference_costs=True), {t_total:.1f} s",
+            "cpu_model": cpu_model()}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def _cpu_worker(args):
