@@ -292,7 +292,10 @@ constexpr int trace_block(int out_layout, int store) {
     return (out_layout == RTPB_AOS && (store & 1)) ? kTraceBlock : 256;
 }
 
-template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE>
+// FEAT: bit 0 = PerfectLens code, bit 1 = RTPB_POLY6 code compiled in.  Leaving out what a plan does
+// not use lowers register pressure (f64 staged: 92 VGPRs without both -> 5 waves/SIMD; 118 with both
+// -> 4), 10-15 % faster when compute-bound.  rtpb_plan::feat picks the variant.
+template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
 __global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 void trace_kernel(TraceArgs<TS> a) {
     constexpr int kB = trace_block(OUT_LAYOUT, STORE);
@@ -330,11 +333,9 @@ void trace_kernel(TraceArgs<TS> a) {
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
     const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
     const cptr<T> table = (cptr<T>)(a.table);
-    T n_cur = material_n<T>(load_material<T>(mats), wl0, table);
+    T n_cur = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats), wl0, table);
     for (int s = 0; s < a.nsurf; ++s) {
-        const T n_next = material_n<T>(load_material<T>(mats + s + 1), wl0, table);
-        Ray<T> at, after;
-        propagate_surface<T>(load_surface<T>(surf + s), r, n_cur, n_next, at, after);
+        const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
         const int p = 2 * s + 1;
         const bool st_at = plane_bit(a.mask_lo, a.mask_hi, p);          // wave-uniform
         const bool st_after = plane_bit(a.mask_lo, a.mask_hi, p + 1);
@@ -342,15 +343,23 @@ void trace_kernel(TraceArgs<TS> a) {
         slot_off += st_at ? a.out_ps : 0;
         const int64_t off_after = slot_off;
         slot_off += st_after ? a.out_ps : 0;
+        // the "at" plane goes to its LDS tile (or straight out) as soon as it is final
+        auto emit_at = [&](const Ray<T>& at) {
+            if constexpr (kStaged) {
+                if (st_at) tile_write<TS>(tile_a, lane, at);
+            } else {
+                if (valid && st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
+            }
+        };
+        Ray<T> after;
+        propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, emit_at, after);
         if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
-            if (st_at) tile_write<TS>(tile_a, lane, at);
             if (st_after) tile_write<TS>(tile_b, lane, after);
             if (st_at || st_after) lds_wait();
             if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
             if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
         } else if (valid) {
-            if (st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
             if (st_after) store_ray<TS, OUT_LAYOUT>(out + off_after, i, a.out_fs, after);
         }
         r = after;
@@ -659,6 +668,7 @@ struct rtpb_plan {
     std::vector<rtpb_material> mats;    // table pointers cleared; see table_off/table_len
     std::vector<int32_t> table_off;
     std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
+    int feat = 0;                       // kernel features needed: 1 = PerfectLens, 2 = POLY6 material
     std::mutex mu;
     void* blob[kMaxDevices] = {};
     size_t off_mats = 0, off_table = 0, blob_bytes = 0;
@@ -752,37 +762,40 @@ std::atomic<int> g_nt_stores{1};
 std::atomic<int> g_waves_per_eu{0};
 std::atomic<int> g_stage_input{0};
 
-template <typename T, int IL, int OL, int ST, int W>
+template <typename T, int IL, int OL, int ST, int W, int FEAT>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
     constexpr int kB = trace_block(OL, ST);
     const int64_t blocks = (a.n + kB - 1) / kB;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W>), dim3(static_cast<unsigned>(blocks)), dim3(kB), 0, st, a);
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), 0, st,
+                       a);
     return hipGetLastError();
 }
 
 template <typename T, int IL, int OL, int ST>
-hipError_t launch_one(const TraceArgs<T>& a, hipStream_t st) {
+hipError_t launch_one(const TraceArgs<T>& a, int feat, hipStream_t st) {
     if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
         const int w = g_waves_per_eu.load();
-        if (w == 5) return launch_w<T, IL, OL, ST, 5>(a, st);
+        if (w == 5) return launch_w<T, IL, OL, ST, 5, 3>(a, st);
     }
-    return launch_w<T, IL, OL, ST, 1>(a, st);
+    if (feat == 0) return launch_w<T, IL, OL, ST, 1, 0>(a, st);
+    if (feat == 1) return launch_w<T, IL, OL, ST, 1, 1>(a, st);
+    return launch_w<T, IL, OL, ST, 1, 3>(a, st);
 }
 
 template <typename T>
-hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, hipStream_t st) {
+hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, int feat, hipStream_t st) {
     const bool staged = g_aos_staging.load() != 0;
     const bool nt = g_nt_stores.load() != 0;
     if (ol == RTPB_AOS) {
         if (!staged)
-            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 0>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 0>(a, st);
-        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<T, RTPB_AOS, RTPB_AOS, 7>(a, st);
+            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 0>(a, feat, st);
+        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<T, RTPB_AOS, RTPB_AOS, 7>(a, feat, st);
         if (nt)
-            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 3>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 3>(a, st);
-        return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 1>(a, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 1>(a, st);
+            return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 3>(a, feat, st);
+        return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 1>(a, feat, st);
     }
-    if (il == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_SOA, 0>(a, st);
-    return launch_one<T, RTPB_SOA, RTPB_SOA, 0>(a, st);
+    if (il == RTPB_AOS) return launch_one<T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
+    return launch_one<T, RTPB_SOA, RTPB_SOA, 0>(a, feat, st);
 }
 
 int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int64_t in_fs, void* out, int ol,
@@ -806,7 +819,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int6
         a.mask_lo = lo;
         a.mask_hi = hi;
         a.nsurf = plan->nsurf;
-        return launch_trace<TS>(a, il, ol, st);
+        return launch_trace<TS>(a, il, ol, plan->feat, st);
     };
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing.on) {
@@ -1003,6 +1016,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
             return fail(RTPB_E_INVALID, "surface " + std::to_string(k) + ": unknown kind");
         }
         p->surf.push_back(surfaces[k]);
+        if (surfaces[k].kind == RTPB_PERFECT_LENS) p->feat |= 1;
     }
     for (int k = 0; k < nmat; ++k) {
         rtpb_material m = materials[k];
@@ -1011,6 +1025,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
             return fail(RTPB_E_INVALID, "material " + std::to_string(k) + ": unknown kind");
         }
         p->table_off.push_back(static_cast<int32_t>(p->table.size() / 2));
+        if (m.kind == RTPB_POLY6) p->feat |= 3;
         if (m.kind == RTPB_TABLE) {
             if (m.table_len <= 0 || !m.table) {
                 delete p;

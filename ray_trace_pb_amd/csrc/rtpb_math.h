@@ -109,7 +109,9 @@ RTPB_HD T np_sign(T v) {
 }
 
 // ------------------------------------------------------------------ Material.n (MAT:39-144)
-template <typename T, typename TablePtr>
+// WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
+// budget); only valid for plans without POLY6 materials (rtpb_plan::lite).
+template <typename T, bool WITH_POLY6 = true, typename TablePtr>
 RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
     switch (m.kind) {
     case CONSTANT:
@@ -125,10 +127,14 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
         return tsqrt<T>(acc + T(1));
     }
     case POLY6: {                                                    // MAT:137-144 (Ebaf11)
-        const T w2 = wl * wl;
-        const T n2 = m.c[0] + m.c[1] * w2 + m.c[2] * tpow<T>(wl, T(-2)) + m.c[3] * tpow<T>(wl, T(-4)) +
-                     m.c[4] * tpow<T>(wl, T(-6)) + m.c[5] * tpow<T>(wl, T(-8));
-        return tsqrt<T>(n2);
+        if constexpr (!WITH_POLY6) {
+            return qnan<T>();
+        } else {
+            const T w2 = wl * wl;
+            const T n2 = m.c[0] + m.c[1] * w2 + m.c[2] * tpow<T>(wl, T(-2)) + m.c[3] * tpow<T>(wl, T(-4)) +
+                         m.c[4] * tpow<T>(wl, T(-6)) + m.c[5] * tpow<T>(wl, T(-8));
+            return tsqrt<T>(n2);
+        }
     }
     default: {                                                       // TABLE: host-evaluated n(lambda)
         // (wavelength, n) pairs sorted by wavelength, NaN keys last (sort_table): binary search for
@@ -292,12 +298,18 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
 
 // ------------------------------------------------------------------ one surface: (at, after)
 // Refracting surfaces RT:1160-1234, reflecting RT:1238-1303, PerfectLens RT:1601-1801.
-template <typename T>
-RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
+// WITH_LENS = false compiles the PerfectLens case out (lower register pressure -> 5 waves/SIMD instead
+// of 4); only valid for plans without PerfectLens surfaces (rtpb_plan::lite).
+// The "at" plane is handed to emit_at as soon as it is final, so the kernel can stage it to LDS before
+// the rest of the surface is computed (the PerfectLens path computes it first: it depends on r only).
+template <typename T, bool WITH_LENS = true, typename EmitAt>
+RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at,
+                                    Ray<T>& after) {
     const int kind = s.kind;
-    if (kind == PERFECT_LENS) {
+    if (WITH_LENS && kind == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
+        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false));   // "before" plane, RT:1790-1793
         const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
         const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
         const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false);
@@ -325,7 +337,6 @@ RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T 
         const T k = T(Const<T>::two_pi) / r.wl;
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
         after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false);
-        at = to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false);
         return;
     }
 
@@ -342,18 +353,23 @@ RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T 
     }
 
     if (kind == PLANE_MIRROR) {
+        emit_at(ri);
         after = reflect(ri, Nx, Ny, Nz);
         if (!on_flat(ri, s)) kill(after);
-        at = ri;
         return;
     }
 
     // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
     if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
+    emit_at(ri);
     after = snell(ri, Nx, Ny, Nz, n1, n2);
     const bool ok = (kind == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
     if (!ok) kill(after);
-    at = ri;
+}
+
+template <typename T, bool WITH_LENS = true>
+RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
+    propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, [&](const Ray<T>& v) { at = v; }, after);
 }
 
 // ------------------------------------------------------------------ host: descriptor lowering
