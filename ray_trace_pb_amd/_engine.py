@@ -11,6 +11,7 @@
   nothing leaves HBM.
 """
 import collections
+import contextlib
 import ctypes
 import threading
 
@@ -120,25 +121,63 @@ def lower_material(m, wavelengths):
 
 
 # ------------------------------------------------------------------------- plan cache
+# Plans (device-resident descriptors) cached by the lowered content, LRU-bounded.  A plan in use by a
+# trace (plan_ref) is never destroyed under it: eviction only marks it, and the last user frees it.
+class _Plan:
+    __slots__ = ("ptr", "lib", "users", "evicted")
+
+    def __init__(self, ptr, lib):
+        self.ptr, self.lib, self.users, self.evicted = ptr, lib, 0, False
+
+
 _PLANS = collections.OrderedDict()
 _PLANS_MAX = 32
 _plans_lock = threading.Lock()
 
 
-def plan_for(low):
+def _acquire(low):
     with _plans_lock:
         p = _PLANS.get(low.key)
         if p is not None:
             _PLANS.move_to_end(low.key)
-            return p
-        out = ctypes.c_void_p()
-        C.check(C.lib().rtpb_plan_create(low.surfaces, low.nsurf, low.materials, low.nsurf + 1, low.dtype,
+        else:
+            out = ctypes.c_void_p()
+            lib = C.lib()
+            C.check(lib.rtpb_plan_create(low.surfaces, low.nsurf, low.materials, low.nsurf + 1, low.dtype,
                                          ctypes.byref(out)))
-        _PLANS[low.key] = out
-        while len(_PLANS) > _PLANS_MAX:
-            _, old = _PLANS.popitem(last=False)
-            C.lib().rtpb_plan_destroy(old)
-        return out
+            p = _Plan(out, lib)
+            _PLANS[low.key] = p
+            while len(_PLANS) > _PLANS_MAX:
+                _, old = _PLANS.popitem(last=False)
+                old.evicted = True
+                if old.users == 0:
+                    old.lib.rtpb_plan_destroy(old.ptr)
+        p.users += 1
+        return p
+
+
+def _release(p):
+    with _plans_lock:
+        p.users -= 1
+        if p.evicted and p.users == 0:
+            p.lib.rtpb_plan_destroy(p.ptr)
+
+
+@contextlib.contextmanager
+def plan_ref(low):
+    """The cached plan of a lowered system, held for the duration of the ``with`` block."""
+    p = _acquire(low)
+    try:
+        yield p.ptr
+    finally:
+        _release(p)
+
+
+def plan_for(low):
+    """The cached plan's raw pointer (single-threaded tools; library paths use plan_ref)."""
+    p = _acquire(low)
+    _release(p)
+    return p.ptr
 
 
 def plane_mask(planes):
@@ -192,7 +231,6 @@ def host_empty(shape, dtype):
 
 def trace_host(low, rays2d, planes, devices=None, out=None):
     """NumPy (N, 8) -> NumPy (len(planes), N, 8)."""
-    plan = plan_for(low)
     rays2d = np.ascontiguousarray(rays2d, dtype=_np_dtype(low.dtype))
     n = rays2d.shape[0]
     if out is None:
@@ -204,14 +242,14 @@ def trace_host(low, rays2d, planes, devices=None, out=None):
     else:
         devs = (ctypes.c_int32 * len(devices))(*devices)
         ndev = len(devices)
-    C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, n, out.ctypes.data, lo, hi, devs, ndev))
+    with plan_ref(low) as plan:
+        C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, n, out.ctypes.data, lo, hi, devs, ndev))
     return out
 
 
 def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None):
     """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA]."""
     import torch
-    plan = plan_for(low)
     tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
     rays = rays.to(dtype=tdt).contiguous()
     n = rays.shape[0]
@@ -221,6 +259,7 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     lo, hi = plane_mask(planes)
     if stream is None:
         stream = torch.cuda.current_stream(rays.device).cuda_stream
-    C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), n, C.RTPB_AOS, 0,
-                               out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+    with plan_ref(low) as plan:
+        C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), n, C.RTPB_AOS, 0,
+                                   out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
     return out

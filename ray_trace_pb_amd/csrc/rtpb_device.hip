@@ -671,20 +671,26 @@ struct rtpb_plan {
     int feat = 0;                       // kernel features needed: 1 = PerfectLens, 2 = POLY6 material
     std::mutex mu;
     void* blob[kMaxDevices] = {};
-    size_t off_mats = 0, off_table = 0, blob_bytes = 0;
+    size_t off_mats = 0, off_table = 0, blob_bytes = 0;   // blob layout, fixed at plan creation
 };
 
 namespace {
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Blob layout: [S surfaces][S+1 materials][table pairs], each part 256-byte aligned.  Computed once at
+// plan creation, so launches on any device read the offsets without synchronisation.
 template <typename T>
-std::vector<unsigned char> build_blob(const rtpb_plan& p, size_t& off_mats, size_t& off_table) {
-    const size_t S = p.surf.size(), M = p.mats.size();
-    off_mats = align256(S * sizeof(DevSurface<T>));
-    off_table = off_mats + align256(M * sizeof(DevMaterial<T>));
-    const size_t bytes = off_table + align256(std::max<size_t>(p.table.size(), 2) * sizeof(T));
-    std::vector<unsigned char> blob(bytes, 0);
+void blob_layout(rtpb_plan& p) {
+    p.off_mats = align256(p.surf.size() * sizeof(DevSurface<T>));
+    p.off_table = p.off_mats + align256(p.mats.size() * sizeof(DevMaterial<T>));
+    p.blob_bytes = p.off_table + align256(std::max<size_t>(p.table.size(), 2) * sizeof(T));
+}
+
+template <typename T>
+std::vector<unsigned char> build_blob(const rtpb_plan& p) {
+    const size_t S = p.surf.size(), M = p.mats.size(), off_mats = p.off_mats, off_table = p.off_table;
+    std::vector<unsigned char> blob(p.blob_bytes, 0);
     auto* ds = reinterpret_cast<DevSurface<T>*>(blob.data());
     for (size_t k = 0; k < S; ++k) {
         const DevSurface<double> d = lower_surface(p.surf[k]);
@@ -722,7 +728,7 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p, size_t& off_mats, size
 int plan_device_blob(rtpb_plan* p, int dev, void** out) {
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->blob[dev]) {
-        std::vector<unsigned char> host = build_blob<double>(*p, p->off_mats, p->off_table);
+        std::vector<unsigned char> host = build_blob<double>(*p);
         DeviceGuard g(dev);
         void* d = nullptr;
         HIP_TRY(hipMalloc(&d, host.size()));
@@ -732,7 +738,6 @@ int plan_device_blob(rtpb_plan* p, int dev, void** out) {
             return fail(RTPB_E_HIP, std::string("hipMemcpy(plan): ") + hipGetErrorString(e));
         }
         p->blob[dev] = d;
-        p->blob_bytes = host.size();
     }
     *out = p->blob[dev];
     return RTPB_OK;
@@ -1041,6 +1046,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
         m.table = nullptr;
         p->mats.push_back(m);
     }
+    blob_layout<double>(*p);
     *plan_out = p;
     return RTPB_OK;
 }

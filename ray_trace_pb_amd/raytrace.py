@@ -435,19 +435,20 @@ def propagate_user_geometry(surface, ray_array, material1, material2, *, devices
     axis = getattr(surface, "input_axis", (0.0, 0.0, 1.0))
     low = E.lower([_AxisOnly(axis)], [material1, material2 if material2 is not None else material1],
                   lambda: E.distinct_wavelengths(h_d[:, 7]), code)
-    plan = E.plan_for(low)
     lib = C.lib()
     stream = torch.cuda.current_stream(dev).cuda_stream
-    if not reflect:                                             # front-side test (RT:1184-1192)
-        r_d = to_dev(rays, 8)
-        C.check(lib.rtpb_front_side(plan, dev.index, r_d.data_ptr(), h_d.data_ptr(), n, h_d.data_ptr(), stream))
-    hits_user = h_d if on_device else h_d.cpu().numpy()
-    on = surface.is_pt_on_surface(hits_user)                    # user hook (RT:1225, 1293)
-    on_t = torch.as_tensor(on if torch.is_tensor(on) else np.asarray(on)).to(dev)
-    on_d = torch.broadcast_to(on_t.reshape(-1) != 0, (n,)).to(torch.uint8).contiguous()
-    out_d = torch.empty_like(h_d)
-    C.check(lib.rtpb_interact(plan, dev.index, C.RTPB_REFLECT if reflect else C.RTPB_REFRACT, h_d.data_ptr(),
-                              n_d.data_ptr(), on_d.data_ptr(), n, out_d.data_ptr(), stream))
+    with E.plan_ref(low) as plan:
+        if not reflect:                                         # front-side test (RT:1184-1192)
+            r_d = to_dev(rays, 8)
+            C.check(lib.rtpb_front_side(plan, dev.index, r_d.data_ptr(), h_d.data_ptr(), n, h_d.data_ptr(),
+                                        stream))
+        hits_user = h_d if on_device else h_d.cpu().numpy()
+        on = surface.is_pt_on_surface(hits_user)                # user hook (RT:1225, 1293)
+        on_t = torch.as_tensor(on if torch.is_tensor(on) else np.asarray(on)).to(dev)
+        on_d = torch.broadcast_to(on_t.reshape(-1) != 0, (n,)).to(torch.uint8).contiguous()
+        out_d = torch.empty_like(h_d)
+        C.check(lib.rtpb_interact(plan, dev.index, C.RTPB_REFLECT if reflect else C.RTPB_REFRACT,
+                                  h_d.data_ptr(), n_d.data_ptr(), on_d.data_ptr(), n, out_d.data_ptr(), stream))
     new = torch.stack((h_d, out_d))
     if on_device:
         return torch.cat((hist.to(new.dtype), new), dim=0)

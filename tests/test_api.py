@@ -1,6 +1,7 @@
 """Host-side API parity with the reference (no GPU): system construction (Doublet, concatenate,
 reverse, paraxial placement), paraxial analysis, ray generators and ray utilities against golden
 values produced by the reference, and the lowering to C-ABI descriptors."""
+import collections
 import json
 import os
 
@@ -206,3 +207,37 @@ def test_user_propagate_detection():
     s = rt.System([MyFlat([0, 0, 0], [0, 0, 1], 1)], [])
     x = np.ones((2, 8))
     assert s.ray_trace(x, mat.Vacuum(), mat.Vacuum()) is x
+
+
+def test_plan_cache_never_frees_a_plan_in_use(monkeypatch):
+    """LRU eviction only marks a plan that a trace holds; the last user frees it (no use-after-free
+    when another thread fills the cache meanwhile).  Library calls are stubbed: no GPU needed."""
+    destroyed, created = [], []
+
+    class FakeLib:
+        def rtpb_plan_create(self, s, ns, m, nm, dt, out):
+            created.append(1)
+            out._obj.value = len(created)
+            return 0
+
+        def rtpb_plan_destroy(self, p):
+            destroyed.append(p.value)
+            return 0
+
+    monkeypatch.setattr(C, "lib", lambda: FakeLib())
+    monkeypatch.setattr(E, "_PLANS", collections.OrderedDict())
+    monkeypatch.setattr(E, "_PLANS_MAX", 2)
+
+    class Low:
+        surfaces = materials = None
+        nsurf, dtype = 1, 0
+
+        def __init__(self, k):
+            self.key = k
+    with E.plan_ref(Low("a")) as pa:
+        E.plan_for(Low("b"))
+        E.plan_for(Low("c"))                 # evicts "a" while it is in use
+        assert pa.value not in destroyed
+    assert destroyed == [pa.value]           # freed by its last user
+    E.plan_for(Low("d"))                     # evicts "b" (unused): freed at once
+    assert len(destroyed) == 2
