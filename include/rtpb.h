@@ -11,7 +11,8 @@
  * (RefractingSurface RT:1160-1234, ReflectingSurface RT:1238-1303, PerfectLens RT:1601-1801 with
  * FlatSurface RT:1306-1347, PlaneMirror RT:1377-1412, SphericalSurface RT:1435-1535), every
  * propagate_ray2plane (RT:241-306) and every Material.n (materials.py:39-144) runs fused in one HIP
- * kernel per launch on gfx950.  The history the reference builds with concatenate (RT:1229-1232) is
+ * kernel per launch on gfx950 (Sellmeier / Constant n(lambda) evaluated in the kernel; other
+ * materials looked up in (wavelength, n) tables the caller evaluated with the material's own code).  The history the reference builds with concatenate (RT:1229-1232) is
  * written plane by plane, straight to its final place in the caller's output buffer.
  *
  * Conventions
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 1
+#define RTPB_ABI_VERSION 2   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0

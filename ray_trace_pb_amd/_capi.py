@@ -11,7 +11,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 1
+RTPB_ABI_VERSION = 2
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
