@@ -211,6 +211,19 @@ int rtpb_intersect_rays(int32_t device, int32_t dtype, const void* ray1, int64_t
 int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t group_size, int64_t n_groups,
                     double* workspace, int64_t workspace_len, double* stats_out, void* stream);
 
+/* Fused spot-diagram sweep (the C5 workload): for every group g the fan
+   get_ray_fan(pt_g, theta_max, n_thetas, wavelength_g, nphis, center_ray) (RT:45-96) is generated,
+   traced through `plan` (final state only) and reduced to the 7 statistics of rtpb_spot_stats -- one
+   kernel, nothing but the statistics reaches HBM.  group_params: HOST, n_groups x {x, y, z, wavelength};
+   ex/ey and the (cos, sin) tables as for rtpb_ray_fan_tables (host).  workspace: device doubles,
+   >= n_groups * ceil(n_thetas*nphis / 256) * 7.  stats_out: device, n_groups x 7.  The statistics are
+   bit-identical to rtpb_ray_fan_tables + rtpb_trace (final plane) + rtpb_spot_stats in the plan's
+   storage type. */
+int rtpb_spot_sweep(const rtpb_plan* plan, int32_t device, int64_t n_groups, const double* group_params,
+                    int64_t n_thetas, int64_t nphis, const double center_ray[3], const double ex[3],
+                    const double ey[3], const double* theta_cos_sin, const double* phi_cos_sin, double* workspace,
+                    int64_t workspace_len, double* stats_out, void* stream);
+
 /* ---- tuning knobs (benchmarks / A-B tests; process-wide) ------------------------------------ */
 /* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.

@@ -60,6 +60,7 @@ SIGNATURES = {
     "rtpb_ray_fan_tables": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P, ctypes.c_double, _P]),
     "rtpb_collimated_rays_tables": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P,
                                                    ctypes.c_double, _P]),
+    "rtpb_spot_sweep": (ctypes.c_int, [_P, _i32, _i64, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _i64, _P, _P]),
     "rtpb_front_side": (ctypes.c_int, [_P, _i32, _P, _P, _i64, _P, _P]),
     "rtpb_interact": (ctypes.c_int, [_P, _i32, _i32, _P, _P, _P, _i64, _P, _P]),
     "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),

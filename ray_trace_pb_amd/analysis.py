@@ -51,12 +51,15 @@ def spot_stats(plane, group_size):
 
 
 def spot_sweep(system, initial_material, final_material, field_points, wavelengths, theta_max, n_thetas, nphis=1,
-               center_ray=(0, 0, 1), device="cuda:0", dtype="float64", groups_per_batch=None):
+               center_ray=(0, 0, 1), device="cuda:0", dtype="float64", groups_per_batch=None, fused=True):
     """Spot diagrams for every (field point, wavelength): a ``get_ray_fan(field, theta_max, n_thetas,
     wavelength, nphis)`` bundle per group, generated, traced (final plane only) and reduced on the GPU.
 
-    Returns (summary dict with arrays shaped (n_fields, n_wavelengths, ...), timing dict).  Groups are
-    processed in batches that reuse the same HBM buffers."""
+    ``fused=True`` (default) runs generation, trace and reduction as ONE kernel per batch of groups
+    (``rtpb_spot_sweep``: no rays touch HBM); ``fused=False`` runs the three steps separately through
+    HBM buffers (``rtpb_ray_fan_tables`` -> ``rtpb_trace`` planes='final' -> ``rtpb_spot_stats``).  Both
+    give bit-identical statistics.  Returns (summary dict with arrays shaped (n_fields, n_wavelengths,
+    ...), timing dict)."""
     import torch
     dev = torch.device(device)
     tdt = torch.float64 if dtype in ("float64", np.float64) else torch.float32
@@ -67,12 +70,15 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
     wavelengths = np.atleast_1d(np.asarray(wavelengths, dtype=float))
     G = field_points.shape[0] * wavelengths.size
     per = n_thetas * nphis
-    if groups_per_batch is None:
-        groups_per_batch = max(1, min(G, (1 << 27) // per))     # ~128M rays in flight
     mats = [initial_material] + list(system.materials) + [final_material]
     low = E.lower(system.surfaces, mats, lambda: np.unique(wavelengths), code)
-    sel = E.resolve_planes("final", len(system.surfaces))
     S = len(system.surfaces)
+    if fused:
+        return _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, dev,
+                                 groups_per_batch)
+    if groups_per_batch is None:
+        groups_per_batch = max(1, min(G, (1 << 27) // per))     # ~128M rays in flight
+    sel = E.resolve_planes("final", len(system.surfaces))
     rays = torch.empty((groups_per_batch * per, 8), dtype=tdt, device=dev)
     out = torch.empty((1, groups_per_batch * per, 8), dtype=tdt, device=dev)
     raw = np.zeros((G, 7))
@@ -90,6 +96,41 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     summ = summarize(raw.reshape(field_points.shape[0], wavelengths.size, 7))
+    return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt}
+
+
+def _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, dev,
+                      groups_per_batch):
+    import torch
+    from .raytrace import _fan_tables
+    c = np.array(center_ray)
+    enx, eny, tcs, pcs = _fan_tables(float(theta_max), int(n_thetas), int(nphis), tuple(c.tolist()), c.dtype.str)
+    nf, nw = field_points.shape[0], wavelengths.size
+    params = np.empty((nf * nw, 4))
+    params[:, 0:3] = np.repeat(field_points, nw, axis=0)          # group = field * nw + wavelength
+    params[:, 3] = np.tile(wavelengths, nf)
+    G = params.shape[0]
+    per = n_thetas * nphis
+    tiles = -(-per // 256)
+    if groups_per_batch is None:
+        groups_per_batch = max(1, min(G, 65535, (1 << 26) // (tiles * 7)))   # workspace <= 512 MB
+    ws = torch.empty(groups_per_batch * tiles * 7, dtype=torch.float64, device=dev)
+    stats = torch.empty((G, 7), dtype=torch.float64, device=dev)
+    vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (c, enx, eny)]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    with E.plan_ref(low) as plan:
+        for b0 in range(0, G, groups_per_batch):
+            b1 = min(G, b0 + groups_per_batch)
+            gp = np.ascontiguousarray(params[b0:b1])
+            C.check(C.lib().rtpb_spot_sweep(plan, dev.index or 0, b1 - b0, gp.ctypes.data, int(n_thetas), int(nphis),
+                                            vec[0].ctypes.data, vec[1].ctypes.data, vec[2].ctypes.data,
+                                            tcs.ctypes.data, pcs.ctypes.data, ws.data_ptr(), ws.numel(),
+                                            stats[b0:b1].data_ptr(), stream))
+        raw = stats.cpu().numpy()
+    dt = time.perf_counter() - t0
+    summ = summarize(raw.reshape(nf, nw, 7))
     return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt}
 
 

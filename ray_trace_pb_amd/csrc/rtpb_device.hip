@@ -560,6 +560,74 @@ __global__ __launch_bounds__(kBlock) void spot_final_kernel(SpotArgs a) {
     if (threadIdx.x < kStats) a.stats[g * kStats + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// Spot-diagram sweep, fused (C5).  Group g is the fan get_ray_fan(pt_g, ..., wl_g)
+// (RT:45-96, same per-ray arithmetic as ray_fan_kernel, angles from the caller's tables); each ray is
+// generated in registers, traced through the plan keeping only its final state, and reduced into the
+// same 256-ray tile partials as spot_partial_kernel.  spot_final_kernel then produces statistics
+// bit-identical to generating, tracing (planes='final') and reducing separately -- without the
+// 3 x 64 B per ray of HBM traffic and the launches in between.
+struct SweepArgs {
+    const DevSurface<double>* __restrict__ surf;
+    const DevMaterial<double>* __restrict__ mats;
+    const double* __restrict__ table;
+    const double2* __restrict__ tab;    // (cos, sin): thetas [n_thetas], then phis [nphis]
+    const double* __restrict__ grp;     // per group: x, y, z, wavelength
+    double* __restrict__ partials;
+    int64_t n_thetas, nphis, gsize, tiles;
+    double c[3], ex[3], ey[3];
+    int32_t nsurf;
+};
+
+template <typename TS>
+__device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
+
+template <typename TS, int FEAT>
+__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.y, tile = blockIdx.x;
+    const int64_t j = tile * kBlock + threadIdx.x;
+    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+    if (j < a.gsize) {
+        const int64_t it = j % a.n_thetas, ip = j / a.n_thetas;
+        const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
+        const double ct = t.x, st = t.y, cp = ph.x, sp = ph.y;
+        const double* gp = a.grp + 4 * g;
+        // the fan ray, rounded to the storage type exactly as a generated-then-loaded ray would be
+        Ray<double> r;
+        r.x = stored<TS>(gp[0]); r.y = stored<TS>(gp[1]); r.z = stored<TS>(gp[2]);
+        r.dx = stored<TS>(a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st);
+        r.dy = stored<TS>(a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st);
+        r.dz = stored<TS>(a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st);
+        r.ph = 0.0;
+        r.wl = stored<TS>(gp[3]);
+        const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
+        const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
+        const cptr<double> table = (cptr<double>)(a.table);
+        const double wl0 = r.wl;
+        double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
+        for (int s = 0; s < a.nsurf; ++s) {
+            const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
+            Ray<double> after;
+            propagate_surface_emit<double, (FEAT & 1) != 0>(load_surface<double>(surf + s), r, n_cur, n_next,
+                                                              [](const Ray<double>&) {}, after);
+            r = after;
+            n_cur = n_next;
+        }
+        const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
+        if (x - x == 0.0 && y - y == 0.0) {
+            v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
+        }
+    }
+    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+}
+
 // propagate_ray2plane (RT:241-306) as a standalone operation: per-ray or broadcast plane normal/center,
 // material n(lambda) from a lowered descriptor, optional exclusion of backward propagation; also
 // returns the propagation parameter t.
@@ -1140,32 +1208,46 @@ namespace {
 // Generator tables on the device: (cos, sin) pairs [n_a] then [n_b].  With host tables (the caller's
 // own np.cos / np.sin / np.linspace values) they are copied; otherwise trig_table_kernel evaluates
 // them with the device's libm (within an ulp of the host's).
+// Per-thread pinned staging buffer for small host->device uploads (tables, per-group parameters): the
+// caller fills it, then upload() copies it to `dev` on `st`.  It is reused once its previous copy has
+// completed, so uploads never synchronise the stream.
+struct PinnedStaging {
+    double* buf = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+
+    int reserve(size_t bytes) {
+        if (done) HIP_TRY(hipEventSynchronize(done));
+        if (!done) HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        if (cap < bytes) {
+            if (buf) HIP_TRY(hipHostFree(buf));
+            buf = nullptr;
+            cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&buf), bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return RTPB_OK;
+    }
+    int upload(void* dev, size_t bytes, hipStream_t st) {
+        HIP_TRY(hipMemcpyAsync(dev, buf, bytes, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(done, st));
+        return RTPB_OK;
+    }
+};
+thread_local PinnedStaging g_pinned;
+
 int gen_tables(double2** tab, int64_t n_a, int64_t n_b, const double* host_a, const double* host_b, int a_pairs,
                const TrigArgs& ta, hipStream_t st) {
     const size_t bytes = size_t(n_a + n_b) * sizeof(double2);
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(tab), bytes, st));
     if (host_a || host_b) {
-        // per-thread pinned staging, reused once its previous copy has completed (no stream sync)
-        thread_local struct Staging {
-            double2* buf = nullptr;
-            size_t cap = 0;
-            hipEvent_t done = nullptr;
-        } sg;
-        if (sg.done) HIP_TRY(hipEventSynchronize(sg.done));
-        if (sg.cap < bytes) {
-            if (sg.buf) HIP_TRY(hipHostFree(sg.buf));
-            sg.buf = nullptr;
-            sg.cap = 0;
-            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sg.buf), bytes, hipHostMallocDefault));
-            sg.cap = bytes;
-        }
-        if (!sg.done) HIP_TRY(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming));
+        int rc = g_pinned.reserve(bytes);
+        if (rc) return rc;
+        double2* h = reinterpret_cast<double2*>(g_pinned.buf);
         for (int64_t j = 0; j < n_a; ++j)
-            sg.buf[j] = a_pairs ? make_double2(host_a[2 * j], host_a[2 * j + 1]) : make_double2(host_a[j], 0.0);
-        for (int64_t j = 0; j < n_b; ++j) sg.buf[n_a + j] = make_double2(host_b[2 * j], host_b[2 * j + 1]);
-        HIP_TRY(hipMemcpyAsync(*tab, sg.buf, bytes, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipEventRecord(sg.done, st));
-        return RTPB_OK;
+            h[j] = a_pairs ? make_double2(host_a[2 * j], host_a[2 * j + 1]) : make_double2(host_a[j], 0.0);
+        for (int64_t j = 0; j < n_b; ++j) h[n_a + j] = make_double2(host_b[2 * j], host_b[2 * j + 1]);
+        return g_pinned.upload(*tab, bytes, st);
     }
     TrigArgs a = ta;
     a.tab = *tab;
@@ -1477,6 +1559,70 @@ int rtpb_front_side(const rtpb_plan* plan, int32_t device, const void* rays, con
 int rtpb_interact(const rtpb_plan* plan, int32_t device, int32_t mode, const void* hits, const void* normals,
                   const uint8_t* on_surface, int64_t n, void* out, void* stream) {
     return hook_launch(plan, device, true, mode, nullptr, hits, normals, on_surface, n, out, stream);
+}
+
+int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, const double* group_params,
+                    int64_t n_thetas, int64_t nphis, const double center_ray[3], const double ex[3],
+                    const double ey[3], const double* theta_cos_sin, const double* phi_cos_sin, double* workspace,
+                    int64_t workspace_len, double* stats_out, void* stream) {
+    auto* plan = const_cast<rtpb_plan*>(plan_c);
+    if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n_groups <= 0 || n_thetas <= 0 || nphis <= 0 || !group_params || !center_ray || !ex || !ey ||
+        !theta_cos_sin || !phi_cos_sin || !workspace || !stats_out)
+        return fail(RTPB_E_INVALID, "bad spot-sweep arguments");
+    const int64_t gsize = n_thetas * nphis;
+    const int64_t tiles = (gsize + kBlock - 1) / kBlock;
+    if (workspace_len < n_groups * tiles * kStats)
+        return fail(RTPB_E_INVALID, "workspace too small: need n_groups * ceil(n_thetas*nphis/256) * 7 doubles");
+    if (tiles > 0x7fffffffll || n_groups > 65535) return fail(RTPB_E_LIMIT, "too many groups or rays per group");
+    DeviceGuard g(device);
+    void* blob = nullptr;
+    rc = plan_device_blob(plan, device, &blob);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // one upload: trig tables then the per-group parameters
+    const size_t ntab = size_t(n_thetas + nphis), bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double);
+    void* dbuf = nullptr;
+    HIP_TRY(hipMallocAsync(&dbuf, bytes, st));
+    rc = g_pinned.reserve(bytes);
+    if (rc) return rc;
+    std::memcpy(g_pinned.buf, theta_cos_sin, size_t(2 * n_thetas) * sizeof(double));
+    std::memcpy(g_pinned.buf + 2 * n_thetas, phi_cos_sin, size_t(2 * nphis) * sizeof(double));
+    std::memcpy(g_pinned.buf + 2 * ntab, group_params, size_t(4 * n_groups) * sizeof(double));
+    rc = g_pinned.upload(dbuf, bytes, st);
+    if (rc) return rc;
+    SweepArgs a{};
+    a.surf = static_cast<const DevSurface<double>*>(blob);
+    a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
+    a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
+    a.tab = static_cast<const double2*>(dbuf);
+    a.grp = reinterpret_cast<const double*>(static_cast<char*>(dbuf) + ntab * sizeof(double2));
+    a.partials = workspace;
+    a.n_thetas = n_thetas;
+    a.nphis = nphis;
+    a.gsize = gsize;
+    a.tiles = tiles;
+    for (int j = 0; j < 3; ++j) {
+        a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
+    }
+    a.nsurf = plan->nsurf;
+    const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(n_groups));
+    auto go = [&](auto tag) {
+        using TS = decltype(tag);
+        if (plan->feat == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
+        else if (plan->feat == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((sweep_kernel<TS, 3>), grid, dim3(kBlock), 0, st, a);
+    };
+    if (plan->dtype == RTPB_F64) go(double{});
+    else go(float{});
+    HIP_TRY(hipGetLastError());
+    SpotArgs sa{nullptr, workspace, stats_out, gsize, n_groups, tiles};
+    hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, sa);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(dbuf, st));
+    return RTPB_OK;
 }
 
 int rtpb_set_tuning(const char* key, int64_t value) {

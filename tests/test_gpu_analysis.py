@@ -90,6 +90,27 @@ def test_spot_sweep_matches_oracle_c5_small():
     assert timing["rays"] == len(fields) * len(wls) * nt * nph
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("case", ["c5", "c2"])
+def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
+    """One-kernel sweep (generate + trace + reduce) == fan kernel + trace(planes='final') + spot stats,
+    bit for bit, for a lens system (C5) and a lens-free one (C2), in both storage types; several
+    batches, ragged group size (not a multiple of 256)."""
+    if case == "c5":
+        system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
+        fields, wls, theta = systems.c5_field_points(2), [0.405, 0.532, 0.785], 0.5 * np.pi / 180
+    else:
+        system, m0, m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
+        fields, wls, theta = [[0.0, 0.0, -5.0], [1.0, -2.0, -5.0]], list(systems.C2_WAVELENGTHS), 0.05
+    args = (system, m0, m1, fields, wls, theta, 301, 77)
+    fu, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=4, fused=True)
+    un, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=5, fused=False)
+    assert fu.keys() == un.keys()
+    for k in fu:
+        assert np.array_equal(fu[k], un[k], equal_nan=True), k
+    assert fu["count"].min() > 0
+
+
 def test_dist_pt2plane_bitwise_vs_reference():
     g = np.load(os.path.join(GOLDEN, "generators.npz"))
     dist, near = rt.dist_pt2plane(g["intersect_in1"][:, :3], np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))
