@@ -302,7 +302,10 @@ void trace_kernel(TraceArgs<TS> a) {
     using T = double;
     constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
     constexpr bool kNT = (STORE & 2) != 0;
-    __shared__ uint4 tiles[kB / 64][2][kTileBytes / 16];  // two tiles per wave: "at" and "after" planes
+    // STORE bit 3: only the final plane is stored (planes='final'): no per-surface store logic, one
+    // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
+    constexpr bool kFinal = (STORE & 8) != 0;
+    __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16];  // per wave: "at" and "after" tiles
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
     const int64_t ray0 = i - lane;                       // first ray of this wave
@@ -313,12 +316,34 @@ void trace_kernel(TraceArgs<TS> a) {
 #endif
     const bool valid = i < a.n;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
-    uint4* tile_b = tiles[threadIdx.x >> 6][1];
+    uint4* tile_b = tiles[threadIdx.x >> 6][kFinal ? 0 : 1];
     Ray<T> r;
     if constexpr (kStaged && IN_LAYOUT == RTPB_AOS && (STORE & 4)) r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
     else r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
     const T wl0 = r.wl;
     TS* __restrict__ out = a.out;
+    const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
+    const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
+    const cptr<T> table = (cptr<T>)(a.table);
+    if constexpr (kFinal) {
+        T n_cur = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats), wl0, table);
+        for (int s = 0; s < a.nsurf; ++s) {
+            const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
+            Ray<T> after;
+            propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next,
+                                                         [](const Ray<T>&) {}, after);
+            r = after;
+            n_cur = n_next;
+        }
+        if constexpr (kStaged) {
+            tile_write<TS>(tile_b, lane, r);
+            lds_wait();
+            tile_flush<TS, kNT>(tile_b, out, ray0, a.n, lane);
+        } else if (valid) {
+            store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
+        }
+        return;
+    }
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
         if constexpr (kStaged) {
@@ -330,9 +355,6 @@ void trace_kernel(TraceArgs<TS> a) {
         }
         slot_off += a.out_ps;
     }
-    const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
-    const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
-    const cptr<T> table = (cptr<T>)(a.table);
     T n_cur = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats), wl0, table);
     for (int s = 0; s < a.nsurf; ++s) {
         const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
@@ -859,6 +881,12 @@ template <typename T>
 hipError_t launch_trace(const TraceArgs<T>& a, int il, int ol, int feat, hipStream_t st) {
     const bool staged = g_aos_staging.load() != 0;
     const bool nt = g_nt_stores.load() != 0;
+    const int last = 2 * a.nsurf;                       // planes='final': only the last plane stored
+    const bool final_only = a.nsurf > 0 && (last < 64 ? (a.mask_lo == (1ull << last) && a.mask_hi == 0)
+                                                      : (a.mask_lo == 0 && a.mask_hi == (1ull << (last - 64))));
+    if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load() &&
+        g_waves_per_eu.load() == 0)
+        return launch_one<T, RTPB_AOS, RTPB_AOS, 11>(a, feat, st);
     if (ol == RTPB_AOS) {
         if (!staged)
             return il == RTPB_AOS ? launch_one<T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st) : launch_one<T, RTPB_SOA, RTPB_AOS, 0>(a, feat, st);
