@@ -7,7 +7,10 @@ import re
 import numpy as np
 import pytest
 
+import ray_trace_pb_amd.materials as mat
+import ray_trace_pb_amd.raytrace as rt
 from ray_trace_pb_amd import _capi as C
+import systems
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "rtpb.h")
@@ -96,3 +99,15 @@ def test_system_ray_trace_raises_without_gpu():
     s = rt.System([rt.FlatSurface([0, 0, 0], [0, 0, 1], 1)], [])
     with pytest.raises(C.RtpbError):
         s.ray_trace(rt.get_collimated_rays([0, 0, -1], 0.5, 3, 0.5), mat.Vacuum(), mat.Vacuum())
+
+
+def test_missing_extension_fails_loudly(monkeypatch, tmp_path):
+    """No silent fallback: without librtpb.so every product call raises (here: a fresh loader pointed
+    at a path with no library)."""
+    monkeypatch.setattr(C, "_lib", None)
+    monkeypatch.setattr(C, "LIB_PATH", str(tmp_path / "librtpb.so"))
+    with pytest.raises(RuntimeError, match="not built"):
+        C.lib()
+    system, rays, m0, m1 = systems.c1_plano_convex(rt, mat)
+    with pytest.raises(RuntimeError, match="not built"):
+        system.ray_trace(rays, m0, m1)
