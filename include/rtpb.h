@@ -224,6 +224,32 @@ int rtpb_spot_sweep(const rtpb_plan* plan, int32_t device, int64_t n_groups, con
                     const double ey[3], const double* theta_cos_sin, const double* phi_cos_sin, double* workspace,
                     int64_t workspace_len, double* stats_out, void* stream);
 
+/* ---- pupil-phase interpolation (scripts/2022_02_06_perfect_imaging_system_psf.py:90-105) */
+/* A 2-D Delaunay triangulation with one value per vertex, in scipy.spatial.Delaunay's representation,
+   plus a uniform cell index (CSR lists of the triangles whose bounding box meets each cell, in
+   increasing triangle order).  All pointers are device pointers. */
+typedef struct rtpb_triangulation {
+    int64_t n_tri;
+    const double* transform;    /* n_tri x 3 x 2: Delaunay.transform (2x2 inverse, then the offset row) */
+    const int32_t* simplices;   /* n_tri x 3 vertex indices */
+    const double* values;       /* value of each vertex */
+    int32_t cells_x, cells_y;   /* cell (cx, cy) covers [x0 + cx*cell_w, +cell_w) x [y0 + cy*cell_h, +cell_h) */
+    double x0, y0, cell_w, cell_h;
+    const int32_t* cell_start;  /* cells_x*cells_y + 1 offsets into cell_tris; cell id = cy*cells_x + cx */
+    const int32_t* cell_tris;
+} rtpb_triangulation;
+
+/* griddata(points, values, (xx, yy), method='linear') on the grid meshgrid(xs, ys) (point (iy, ix) =
+   (xs[ix], ys[iy]), row-major), with scipy's LinearNDInterpolator arithmetic: the first triangle whose
+   barycentric coordinates lie in [-eps, 1+eps] (eps = 100 DBL_EPSILON), c0/c1 from the transform and
+   c2 = (1 - c0) - c1, value = ((0 + c0 v0) + c1 v1) + c2 v2; NaN outside the hull.  Optionally fused
+   with the pupil field of the script: field = exp(i phase), 0 where phase is NaN or
+   sqrt(x^2 + y^2) > radius.  phase_out (ny*nx doubles) and/or field_out (ny*nx interleaved complex
+   doubles) may be NULL.  xs, ys: device arrays. */
+int rtpb_grid_interpolate(int32_t device, const rtpb_triangulation* tri, const double* xs, int64_t nx,
+                          const double* ys, int64_t ny, double radius, double* phase_out, double* field_out,
+                          void* stream);
+
 /* ---- tuning knobs (benchmarks / A-B tests; process-wide) ------------------------------------ */
 /* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.

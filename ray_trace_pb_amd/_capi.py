@@ -31,6 +31,13 @@ class Surface(ctypes.Structure):
                 ("focal_len", ctypes.c_double), ("sin_alpha", ctypes.c_double), ("on_tol", ctypes.c_double)]
 
 
+class Triangulation(ctypes.Structure):
+    _fields_ = [("n_tri", ctypes.c_int64), ("transform", ctypes.c_void_p), ("simplices", ctypes.c_void_p),
+                ("values", ctypes.c_void_p), ("cells_x", ctypes.c_int32), ("cells_y", ctypes.c_int32),
+                ("x0", ctypes.c_double), ("y0", ctypes.c_double), ("cell_w", ctypes.c_double),
+                ("cell_h", ctypes.c_double), ("cell_start", ctypes.c_void_p), ("cell_tris", ctypes.c_void_p)]
+
+
 class Material(ctypes.Structure):
     """struct rtpb_material"""
     _fields_ = [("kind", ctypes.c_int32), ("table_len", ctypes.c_int32), ("c", _c6),
@@ -61,6 +68,8 @@ SIGNATURES = {
     "rtpb_collimated_rays_tables": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P,
                                                    ctypes.c_double, _P]),
     "rtpb_spot_sweep": (ctypes.c_int, [_P, _i32, _i64, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _i64, _P, _P]),
+    "rtpb_grid_interpolate": (ctypes.c_int, [_i32, ctypes.POINTER(Triangulation), _P, _i64, _P, _i64,
+                                             ctypes.c_double, _P, _P, _P]),
     "rtpb_front_side": (ctypes.c_int, [_P, _i32, _P, _P, _i64, _P, _P]),
     "rtpb_interact": (ctypes.c_int, [_P, _i32, _i32, _P, _P, _P, _i64, _P, _P]),
     "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),

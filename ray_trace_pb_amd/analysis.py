@@ -139,8 +139,87 @@ def _fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray, code)
     fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray)
 
 
+class GridInterpolator:
+    """``scipy.interpolate.griddata(points, values, grid, method='linear')`` evaluated on the GPU.
+
+    The Delaunay triangulation is scipy's own (``scipy.spatial.Delaunay``, host, the same call
+    LinearNDInterpolator makes); a uniform cell index of triangle bounding boxes is built once, and
+    ``rtpb_grid_interpolate`` locates and interpolates every grid point with scipy's barycentric
+    arithmetic.  Values for points strictly inside a triangle are bit-identical to scipy's; on a shared
+    edge (within scipy's eps) the first listed triangle is used, which can differ from scipy's walk by a
+    rounding.  ``set_values`` swaps the vertex values (the PSF loop re-uses one triangulation while
+    only the phases change)."""
+
+    def __init__(self, points, device="cuda:0"):
+        import torch
+        from scipy.spatial import Delaunay
+        self.dev = torch.device(device)
+        self.points = np.ascontiguousarray(points, dtype=np.float64)
+        tri = Delaunay(self.points)
+        simp = np.ascontiguousarray(tri.simplices, dtype=np.int32)
+        v = self.points[simp]                                       # (n_tri, 3, 2)
+        lo, hi = v.min(axis=1), v.max(axis=1)
+        span = float(max(np.ptp(self.points[:, 0]), np.ptp(self.points[:, 1]), 1e-300))
+        lo, hi = lo - 1e-9 * span, hi + 1e-9 * span                 # scipy accepts points within eps
+        x0, y0 = lo.min(axis=0)
+        nt = simp.shape[0]
+        ncell = max(1, int(np.sqrt(2 * nt)))
+        cw = max((hi[:, 0].max() - x0) / ncell, 1e-300) * (1 + 1e-12)
+        ch = max((hi[:, 1].max() - y0) / ncell, 1e-300) * (1 + 1e-12)
+        cx0 = np.clip(((lo[:, 0] - x0) / cw).astype(np.int64), 0, ncell - 1)
+        cx1 = np.clip(((hi[:, 0] - x0) / cw).astype(np.int64), 0, ncell - 1)
+        cy0 = np.clip(((lo[:, 1] - y0) / ch).astype(np.int64), 0, ncell - 1)
+        cy1 = np.clip(((hi[:, 1] - y0) / ch).astype(np.int64), 0, ncell - 1)
+        nxs, nys = cx1 - cx0 + 1, cy1 - cy0 + 1
+        cnt = nxs * nys
+        tri_id = np.repeat(np.arange(nt, dtype=np.int64), cnt)
+        local = np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+        cx = np.repeat(cx0, cnt) + local % np.repeat(nxs, cnt)
+        cy = np.repeat(cy0, cnt) + local // np.repeat(nxs, cnt)
+        cell = cy * ncell + cx
+        order = np.lexsort((tri_id, cell))                        # by cell, then triangle index
+        cell, tri_id = cell[order], tri_id[order]
+        start = np.searchsorted(cell, np.arange(ncell * ncell + 1)).astype(np.int32)
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev, dtype=dt)  # noqa: E731
+        self._transform = t(tri.transform.reshape(nt, 6), torch.float64)
+        self._simplices = t(simp, torch.int32)
+        self._start = t(start, torch.int32)
+        self._cells = t(tri_id.astype(np.int32), torch.int32)
+        self._values = torch.zeros(self.points.shape[0], dtype=torch.float64, device=self.dev)
+        self.desc = C.Triangulation(nt, self._transform.data_ptr(), self._simplices.data_ptr(),
+                                    self._values.data_ptr(), ncell, ncell, float(x0), float(y0), float(cw),
+                                    float(ch), self._start.data_ptr(), self._cells.data_ptr())
+
+    def set_values(self, values):
+        import torch
+        self._values.copy_(torch.as_tensor(np.ascontiguousarray(values, dtype=np.float64)))
+        return self
+
+    def __call__(self, xs, ys, radius=None, phase=True):
+        """Interpolate on meshgrid(xs, ys) -> torch (len(ys), len(xs)) phase (NaN outside the hull);
+        with ``radius``, also the pupil field exp(i*phase) (0 outside ``radius`` or where undefined)."""
+        import torch
+        gx = torch.as_tensor(np.ascontiguousarray(xs, dtype=np.float64)).to(self.dev)
+        gy = torch.as_tensor(np.ascontiguousarray(ys, dtype=np.float64)).to(self.dev)
+        nx, ny = gx.numel(), gy.numel()
+        ph = torch.empty((ny, nx), dtype=torch.float64, device=self.dev) if phase else None
+        fld = torch.empty((ny, nx), dtype=torch.complex128, device=self.dev) if radius is not None else None
+        C.check(C.lib().rtpb_grid_interpolate(self.dev.index or 0, C.ctypes.byref(self.desc), gx.data_ptr(), nx,
+                                              gy.data_ptr(), ny, float(radius) if radius is not None else 0.0,
+                                              ph.data_ptr() if ph is not None else None,
+                                              fld.data_ptr() if fld is not None else None,
+                                              torch.cuda.current_stream(self.dev).cuda_stream))
+        return ph, fld
+
+
+def griddata_linear(points, values, xs, ys, device="cuda:0"):
+    """scipy.interpolate.griddata(points, values, meshgrid(xs, ys), method='linear') on the GPU
+    (torch (len(ys), len(xs)); see :class:`GridInterpolator`)."""
+    return GridInterpolator(points, device).set_values(values)(xs, ys)[0]
+
+
 def pupil_psf(system, initial_material, final_material, source_points, wavelength, theta_max, n_thetas, nphis,
-              pupil_plane, pupil_radius, grid_step, grid_extent=3.0, device="cuda:0"):
+              pupil_plane, pupil_radius, grid_step, grid_extent=3.0, device="cuda:0", interp="gpu", as_numpy=True):
     """Point-spread functions from pupil phases (the pipeline of
     scripts/2022_02_06_perfect_imaging_system_psf.py:73-105).
 
@@ -150,7 +229,12 @@ def pupil_psf(system, initial_material, final_material, source_points, wavelengt
     ``scipy.interpolate.griddata`` (linear, Delaunay -- as the script; host), masked outside
     ``pupil_radius`` and where undefined, and Fourier transformed on the GPU (torch.fft = hipFFT):
     E_out = fftshift(fft2(ifftshift(exp(i phi)))).  Returns (psf |E_out|^2 normalised to the stack
-    maximum, pupil field, grid coordinates)."""
+    maximum, pupil field, grid coordinates).
+
+    ``interp='gpu'`` (default) interpolates and forms the pupil field on the GPU
+    (:class:`GridInterpolator`, scipy's triangulation and arithmetic; the triangulation is re-used while
+    the pupil positions stay the same); ``interp='host'`` calls scipy's griddata as the script does.
+    ``as_numpy=False`` returns the psf and pupil stacks as torch CUDA tensors (no host copies)."""
     import torch
     from scipy.interpolate import griddata
     from .raytrace import get_ray_fan
@@ -162,18 +246,33 @@ def pupil_psf(system, initial_material, final_material, source_points, wavelengt
     xx, yy = np.meshgrid(xs, xs)
     interp_pts = np.stack((xx.ravel(), yy.ravel()), axis=1)
     outside = np.sqrt(xx ** 2 + yy ** 2) > pupil_radius
-    pupil = np.zeros((len(src), nxy, nxy), dtype=complex)
-    for ii, p in enumerate(src):
-        rays = get_ray_fan(p, theta_max, n_thetas, wavelength, nphis=nphis, device=dev)
-        plane = system.ray_trace(rays, initial_material, final_material, planes=[pupil_plane])[0]
-        h = plane.cpu().numpy()
-        ok = ~np.isnan(h[:, 0]) & ~np.isnan(h[:, 1])
-        phis = griddata(h[ok, :2], h[ok, 6], interp_pts).reshape(xx.shape)
-        e = np.exp(1j * phis)
-        e[outside] = 0
-        e[np.isnan(phis)] = 0
-        pupil[ii] = e
-    pt = torch.from_numpy(pupil).to(dev)
+    if interp == "gpu":
+        pt = torch.empty((len(src), nxy, nxy), dtype=torch.complex128, device=dev)
+        gi, key = None, None
+        for ii, p in enumerate(src):
+            rays = get_ray_fan(p, theta_max, n_thetas, wavelength, nphis=nphis, device=dev)
+            plane = system.ray_trace(rays, initial_material, final_material, planes=[pupil_plane])[0]
+            h = plane.cpu().numpy()
+            ok = ~np.isnan(h[:, 0]) & ~np.isnan(h[:, 1])
+            pts = np.ascontiguousarray(h[ok, :2])
+            if gi is None or key != pts.tobytes():                  # same pupil positions: same triangulation
+                gi, key = GridInterpolator(pts, dev), pts.tobytes()
+            _, pt[ii] = gi.set_values(h[ok, 6])(xs, xs, radius=pupil_radius, phase=False)
+        pupil = pt.cpu().numpy() if as_numpy else pt
+    else:
+        pupil = np.zeros((len(src), nxy, nxy), dtype=complex)
+        for ii, p in enumerate(src):
+            rays = get_ray_fan(p, theta_max, n_thetas, wavelength, nphis=nphis, device=dev)
+            plane = system.ray_trace(rays, initial_material, final_material, planes=[pupil_plane])[0]
+            h = plane.cpu().numpy()
+            ok = ~np.isnan(h[:, 0]) & ~np.isnan(h[:, 1])
+            phis = griddata(h[ok, :2], h[ok, 6], interp_pts).reshape(xx.shape)
+            e = np.exp(1j * phis)
+            e[outside] = 0
+            e[np.isnan(phis)] = 0
+            pupil[ii] = e
+        pt = torch.from_numpy(pupil).to(dev)
     out = torch.fft.fftshift(torch.fft.fft2(torch.fft.ifftshift(pt, dim=(-2, -1))), dim=(-2, -1))
-    psf = (out.abs() ** 2).cpu().numpy()
-    return psf / psf.max(), pupil, xs
+    psf = out.abs() ** 2
+    psf = psf / psf.max()
+    return (psf.cpu().numpy() if as_numpy else psf), pupil, xs

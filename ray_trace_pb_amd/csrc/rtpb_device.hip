@@ -650,6 +650,52 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
+__global__ __launch_bounds__(kBlock) void grid_interp_kernel(rtpb_triangulation t, const double* __restrict__ xs,
+                                                             int64_t nx, const double* __restrict__ ys, int64_t ny,
+                                                             double radius, double* __restrict__ phase_out,
+                                                             double* __restrict__ field_out) {
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (k >= nx * ny) return;
+    const int64_t iy = k / nx, ix = k % nx;
+    const double x = xs[ix], y = ys[iy];
+    constexpr double eps = 100.0 * 2.220446049250313e-16;      // scipy qhull: 100 * DBL_EPSILON
+    double phase = __builtin_nan("");
+    const double fx = (x - t.x0) / t.cell_w, fy = (y - t.y0) / t.cell_h;
+    if (fx >= 0.0 && fy >= 0.0 && fx < double(t.cells_x) && fy < double(t.cells_y)) {
+        const int64_t cell = int64_t(fy) * t.cells_x + int64_t(fx);
+        for (int32_t q = t.cell_start[cell]; q < t.cell_start[cell + 1]; ++q) {
+            const int32_t s = t.cell_tris[q];
+            const double* T = t.transform + 6 * int64_t(s);
+            // scipy/spatial/_qhull.pyx _barycentric_inside / _barycentric_coordinates (ndim = 2)
+            double c0 = 0.0;
+            c0 += T[0] * (x - T[4]);
+            c0 += T[1] * (y - T[5]);
+            double c1 = 0.0;
+            c1 += T[2] * (x - T[4]);
+            c1 += T[3] * (y - T[5]);
+            const double c2 = (1.0 - c0) - c1;
+            if (!(-eps <= c0 && c0 <= 1.0 + eps) || !(-eps <= c1 && c1 <= 1.0 + eps) ||
+                !(-eps <= c2 && c2 <= 1.0 + eps))
+                continue;
+            // scipy/interpolate/_interpnd.pyx LinearNDInterpolator._do_evaluate
+            const int32_t* v = t.simplices + 3 * int64_t(s);
+            double o = 0.0;
+            o = o + c0 * t.values[v[0]];
+            o = o + c1 * t.values[v[1]];
+            o = o + c2 * t.values[v[2]];
+            phase = o;
+            break;
+        }
+    }
+    if (phase_out) phase_out[k] = phase;
+    if (field_out) {
+        const bool off = sqrt(x * x + y * y) > radius || phase != phase;
+        field_out[2 * k] = off ? 0.0 : cos(phase);
+        field_out[2 * k + 1] = off ? 0.0 : sin(phase);
+    }
+}
+
 // propagate_ray2plane (RT:241-306) as a standalone operation: per-ray or broadcast plane normal/center,
 // material n(lambda) from a lowered descriptor, optional exclusion of backward propagation; also
 // returns the propagation parameter t.
@@ -1650,6 +1696,25 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, sa);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFreeAsync(dbuf, st));
+    return RTPB_OK;
+}
+
+int rtpb_grid_interpolate(int32_t device, const rtpb_triangulation* tri, const double* xs, int64_t nx,
+                          const double* ys, int64_t ny, double radius, double* phase_out, double* field_out,
+                          void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (!tri || !xs || !ys || nx <= 0 || ny <= 0) return fail(RTPB_E_INVALID, "bad grid-interpolate arguments");
+    if (tri->n_tri < 0 || (tri->n_tri > 0 && (!tri->transform || !tri->simplices || !tri->values)) ||
+        tri->cells_x <= 0 || tri->cells_y <= 0 || !tri->cell_start || !tri->cell_tris || !(tri->cell_w > 0.0) ||
+        !(tri->cell_h > 0.0))
+        return fail(RTPB_E_INVALID, "bad triangulation descriptor");
+    if (!phase_out && !field_out) return RTPB_OK;
+    DeviceGuard g(device);
+    const int64_t total = nx * ny;
+    hipLaunchKernelGGL(grid_interp_kernel, dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, static_cast<hipStream_t>(stream), *tri, xs, nx, ys, ny, radius, phase_out, field_out);
+    HIP_TRY(hipGetLastError());
     return RTPB_OK;
 }
 

@@ -142,7 +142,35 @@ def test_propagate_ray2plane_device_bitwise_vs_oracle(exclude):
     assert t_out.is_cuda and t_ts.is_cuda
 
 
-def test_pupil_psf_matches_host_pipeline():
+@pytest.mark.parametrize("layout", ["scattered", "polar_fan"])
+def test_gpu_griddata_matches_scipy(layout):
+    """GridInterpolator == scipy.interpolate.griddata(method='linear'): same NaN (outside-hull) mask,
+    bit-identical values except where a grid point sits on a shared triangle edge (within scipy's eps),
+    which may differ by a rounding."""
+    from scipy.interpolate import griddata
+    rng = np.random.default_rng(3)
+    if layout == "scattered":
+        pts = rng.uniform(-2, 2, (2000, 2))
+    else:                                   # a ray fan seen in a pupil: rings x spokes, incl. y = 0 spokes
+        th, ph = np.meshgrid(np.linspace(-1, 1, 61), np.arange(37) * 2 * np.pi / 37)
+        r = 2.0 * np.sin(1.1 * th) / np.sin(1.1)
+        pts = np.stack((r * np.cos(ph), r * np.sin(ph)), axis=-1).reshape(-1, 2)
+    vals = 1e4 + 3.0 * pts[:, 0] ** 2 - 2.0 * pts[:, 1] + rng.normal(scale=1e-3, size=len(pts))
+    xs = 0.013 * np.arange(401)
+    xs -= xs.mean()
+    ys = xs[::2].copy()
+    got = analysis.griddata_linear(pts, vals, xs, ys, device=DEV).cpu().numpy()
+    xx, yy = np.meshgrid(xs, ys)
+    ref = griddata(pts, vals, np.stack((xx.ravel(), yy.ravel()), 1)).reshape(xx.shape)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    fin = ~np.isnan(ref)
+    assert fin.sum() > 10000
+    assert (got[fin] == ref[fin]).mean() > 0.99
+    assert np.max(np.abs(got[fin] - ref[fin])) <= 1e-12 * np.max(np.abs(ref[fin]))
+
+
+@pytest.mark.parametrize("interp", ["gpu", "host"])
+def test_pupil_psf_matches_host_pipeline(interp):
     """§8f #4: GPU trace + griddata + GPU FFT vs the reference script's NumPy pipeline on the oracle."""
     from numpy import fft
     from scipy.interpolate import griddata
@@ -157,7 +185,7 @@ def test_pupil_psf_matches_host_pipeline():
                        [mat.Vacuum(), mat.Vacuum(), mat.Vacuum()])
     srcs = [[0, 0, -1e-4], [0, 0, 0], [0, 0, 1e-4]]
     psf, pupil, xs = analysis.pupil_psf(system, mat.Constant(n1), mat.Vacuum(), srcs, wavelength, alpha, 41, 21,
-                                        pupil_plane=4, pupil_radius=r1, grid_step=0.05, device=DEV)
+                                        pupil_plane=4, pupil_radius=r1, grid_step=0.05, device=DEV, interp=interp)
     S = [surface_to_dict(s) for s in system.surfaces]
     M = [material_to_dict(m) for m in [mat.Constant(n1)] + list(system.materials) + [mat.Vacuum()]]
     xx, yy = np.meshgrid(xs, xs)
