@@ -603,18 +603,23 @@ struct SweepArgs {
 template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
 
+// Two rays per lane: block b covers tiles 2b and 2b+1 of its group; both rays go through each surface
+// in one straight-line region (propagate_surface_pair) so two independent dependency chains
+// interleave (-6 % vs one ray per lane); each tile is reduced separately, with the same tree as
+// spot_partial_kernel.
 template <typename TS, int FEAT>
 __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     __shared__ double red[kStats][kBlock];
-    const int64_t g = blockIdx.y, tile = blockIdx.x;
-    const int64_t j = tile * kBlock + threadIdx.x;
-    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
-    if (j < a.gsize) {
-        const int64_t it = j % a.n_thetas, ip = j / a.n_thetas;
+    const int64_t g = blockIdx.y;
+    const int64_t tileA = 2 * int64_t(blockIdx.x), tileB = tileA + 1;
+    const int64_t jA = tileA * kBlock + threadIdx.x, jB = tileB * kBlock + threadIdx.x;
+    const bool okA = jA < a.gsize, okB = jB < a.gsize;
+    const double* gp = a.grp + 4 * g;
+    auto gen = [&](int64_t j) {
+        const int64_t jj = j < a.gsize ? j : 0;
+        const int64_t it = jj % a.n_thetas, ip = jj / a.n_thetas;
         const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
         const double ct = t.x, st = t.y, cp = ph.x, sp = ph.y;
-        const double* gp = a.grp + 4 * g;
-        // the fan ray, rounded to the storage type exactly as a generated-then-loaded ray would be
         Ray<double> r;
         r.x = stored<TS>(gp[0]); r.y = stored<TS>(gp[1]); r.z = stored<TS>(gp[2]);
         r.dx = stored<TS>(a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st);
@@ -622,32 +627,44 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
         r.dz = stored<TS>(a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st);
         r.ph = 0.0;
         r.wl = stored<TS>(gp[3]);
-        const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
-        const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
-        const cptr<double> table = (cptr<double>)(a.table);
-        const double wl0 = r.wl;
-        double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
-        for (int s = 0; s < a.nsurf; ++s) {
-            const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
-            Ray<double> after;
-            propagate_surface_emit<double, (FEAT & 1) != 0>(load_surface<double>(surf + s), r, n_cur, n_next,
-                                                              [](const Ray<double>&) {}, after);
-            r = after;
-            n_cur = n_next;
-        }
-        const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
-        if (x - x == 0.0 && y - y == 0.0) {
-            v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
-        }
+        return r;
+    };
+    Ray<double> rA = gen(jA), rB = gen(jB);
+    const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
+    const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
+    const cptr<double> table = (cptr<double>)(a.table);
+    const double wl0 = rA.wl;                          // one wavelength per group
+    double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
+    for (int s = 0; s < a.nsurf; ++s) {
+        const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
+        const DevSurface<double> sd = load_surface<double>(surf + s);
+        Ray<double> aA, aB;
+        propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, aA, aB);
+        rA = aA;
+        rB = aB;
+        n_cur = n_next;
     }
-    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
-    __syncthreads();
-    for (int w = kBlock / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
+        double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+        if (ok) {
+            const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
+            if (x - x == 0.0 && y - y == 0.0) {
+                v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
+            }
+        }
+        for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
         __syncthreads();
-    }
-    if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+        for (int w = kBlock / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w)
+                for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x < kStats && tile < a.tiles)
+            a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+        __syncthreads();
+    };
+    reduce(rA, okA, tileA);
+    reduce(rB, okB, tileB);
 }
 
 // griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
@@ -1682,7 +1699,7 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
     }
     a.nsurf = plan->nsurf;
-    const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(n_groups));
+    const dim3 grid(static_cast<unsigned>((tiles + 1) / 2), static_cast<unsigned>(n_groups));
     auto go = [&](auto tag) {
         using TS = decltype(tag);
         if (plan->feat == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);

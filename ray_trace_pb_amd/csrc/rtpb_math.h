@@ -298,15 +298,12 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
 
 // ------------------------------------------------------------------ one surface: (at, after)
 // Refracting surfaces RT:1160-1234, reflecting RT:1238-1303, PerfectLens RT:1601-1801.
-// WITH_LENS = false compiles the PerfectLens case out (lower register pressure -> 5 waves/SIMD instead
-// of 4); only valid for plans without PerfectLens surfaces (rtpb_plan::lite).
-// The "at" plane is handed to emit_at as soon as it is final, so the kernel can stage it to LDS before
-// the rest of the surface is computed (the PerfectLens path computes it first: it depends on r only).
-template <typename T, bool WITH_LENS = true, typename EmitAt>
-RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at,
-                                    Ray<T>& after) {
-    const int kind = s.kind;
-    if (WITH_LENS && kind == PERFECT_LENS) {
+// One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
+// handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
+// surface is computed (the PerfectLens path computes it first: it depends on r only).
+template <typename T, int KIND, typename EmitAt>
+RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at, Ray<T>& after) {
+    if constexpr (KIND == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
         emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false));   // "before" plane, RT:1790-1793
@@ -337,34 +334,66 @@ RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n
         const T k = T(Const<T>::two_pi) / r.wl;
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
         after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false);
-        return;
+    } else {
+        T Nx, Ny, Nz;
+        Ray<T> ri;
+        if constexpr (KIND == SPHERE) {
+            ri = sphere_hit(r, s, n1);
+            Nx = (ri.x - s.c[0]) / s.R;                                   // RT:1476
+            Ny = (ri.y - s.c[1]) / s.R;
+            Nz = (ri.z - s.c[2]) / s.R;
+        } else {                                                           // FLAT, PLANE_MIRROR
+            Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
+            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true);   // RT:1331-1337, 1398-1403
+        }
+        if constexpr (KIND == PLANE_MIRROR) {
+            emit_at(ri);
+            after = reflect(ri, Nx, Ny, Nz);
+            if (!on_flat(ri, s)) kill(after);
+        } else {
+            // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
+            if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
+            emit_at(ri);
+            after = snell(ri, Nx, Ny, Nz, n1, n2);
+            const bool ok = (KIND == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
+            if (!ok) kill(after);
+        }
     }
+}
 
-    T Nx, Ny, Nz;
-    Ray<T> ri;
-    if (kind == SPHERE) {
-        ri = sphere_hit(r, s, n1);
-        Nx = (ri.x - s.c[0]) / s.R;                                   // RT:1476
-        Ny = (ri.y - s.c[1]) / s.R;
-        Nz = (ri.z - s.c[2]) / s.R;
-    } else {                                                           // FLAT, PLANE_MIRROR
-        Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-        ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true);   // RT:1331-1337, 1398-1403
+// Any surface: a wave-uniform switch on the kind.  WITH_LENS = false compiles the PerfectLens case out
+// (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans without PerfectLens
+// surfaces (rtpb_plan::feat).
+template <typename T, bool WITH_LENS = true, typename EmitAt>
+RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at,
+                                    Ray<T>& after) {
+    const int kind = s.kind;
+    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, emit_at, after);
+    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, emit_at, after);
+    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, emit_at, after);
+    else surface_step<T, FLAT>(s, r, n1, n2, emit_at, after);
+}
+
+// Two independent rays through the same surface: one kind dispatch, both bodies in one straight-line
+// region so the scheduler can interleave their dependency chains.
+template <typename T, bool WITH_LENS = true>
+RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, const Ray<T>& rb, T n1, T n2,
+                                    Ray<T>& after_a, Ray<T>& after_b) {
+    auto none = [](const Ray<T>&) {};
+    const int kind = s.kind;
+    if (WITH_LENS && kind == PERFECT_LENS) {
+        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, none, after_a);
+        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, none, after_b);
+    } else if (kind == SPHERE) {
+        surface_step<T, SPHERE>(s, ra, n1, n2, none, after_a);
+        surface_step<T, SPHERE>(s, rb, n1, n2, none, after_b);
+    } else if (kind == PLANE_MIRROR) {
+        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, none, after_a);
+        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, none, after_b);
+    } else {
+        surface_step<T, FLAT>(s, ra, n1, n2, none, after_a);
+        surface_step<T, FLAT>(s, rb, n1, n2, none, after_b);
     }
-
-    if (kind == PLANE_MIRROR) {
-        emit_at(ri);
-        after = reflect(ri, Nx, Ny, Nz);
-        if (!on_flat(ri, s)) kill(after);
-        return;
-    }
-
-    // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
-    if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
-    emit_at(ri);
-    after = snell(ri, Nx, Ny, Nz, n1, n2);
-    const bool ok = (kind == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
-    if (!ok) kill(after);
 }
 
 template <typename T, bool WITH_LENS = true>
