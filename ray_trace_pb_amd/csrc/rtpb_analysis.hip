@@ -1,0 +1,366 @@
+// rtpb_analysis.hip -- device analysis around the trace: intersect_rays
+// (RT:164-238), per-group spot statistics, the fused spot-diagram sweep (generate + trace + reduce),
+// and griddata-style interpolation of pupil phases onto a grid.
+#include "rtpb_internal.h"
+
+using namespace rtpbi;
+
+namespace {
+
+// intersect_rays (RT:164-238): closest-approach solve from the first non-singular 2x2 sub-system,
+// verified to 1e-12.  NaN determinants count as "non-zero" exactly like numpy's truthiness.
+struct IsectArgs {
+    const void* __restrict__ r1;
+    const void* __restrict__ r2;
+    void* __restrict__ out;
+    int64_t n, n1, n2;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void intersect_kernel(IsectArgs a) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const T* p = static_cast<const T*>(a.r1) + (a.n1 == 1 ? 0 : i) * 8;
+    const T* q = static_cast<const T*>(a.r2) + (a.n2 == 1 ? 0 : i) * 8;
+    const double x1 = p[0], y1 = p[1], z1 = p[2], dx1 = p[3], dy1 = p[4], dz1 = p[5];
+    const double x2 = q[0], y2 = q[1], z2 = q[2], dx2 = q[3], dy2 = q[4], dz2 = q[5];
+    const double nan = qnan<double>();
+    const double det_xz = dx2 * dz1 - dz2 * dx1, det_xy = dx2 * dy1 - dy2 * dx1, det_yz = dz2 * dy1 - dy2 * dz1;
+    double s = nan;
+    if (det_xz != 0.0) s = ((z2 - z1) * dx1 - (x2 - x1) * dz1) / det_xz;
+    else if (det_xy != 0.0) s = ((y2 - y1) * dx1 - (x2 - x1) * dy1) / det_xy;
+    else if (det_yz != 0.0) s = ((y2 - y1) * dz1 - (z2 - z1) * dy1) / det_yz;
+    double t;
+    if (dz1 != 0.0) t = (z2 + s * dz2 - z1) / dz1;
+    else if (dy1 != 0.0) t = (y2 + s * dy2 - y1) / dy1;
+    else t = (x2 + s * dx2 - x1) / dx1;
+    double o[3] = {x1 + t * dx1, y1 + t * dy1, z1 + t * dz1};
+    const double e[3] = {o[0] - (x2 + s * dx2), o[1] - (y2 + s * dy2), o[2] - (z2 + s * dz2)};
+    // numpy.max over the 3 |differences| propagates NaN, and NaN > 1e-12 is false
+    double m = tabs(e[0]);
+    for (int k = 1; k < 3; ++k) {
+        const double v = tabs(e[k]);
+        if (is_nan(m)) break;
+        if (is_nan(v) || v > m) m = v;
+    }
+    if (m > 1e-12) o[0] = o[1] = o[2] = nan;
+    T* out = static_cast<T*>(a.out) + i * 3;
+    out[0] = T(o[0]); out[1] = T(o[1]); out[2] = T(o[2]);
+}
+
+// Spot statistics of one history plane, per contiguous group of `gsize` rays (per
+// (field, wavelength) spot diagrams).  Rays whose x or y is not finite are skipped.  Deterministic:
+// pass 1 reduces each 256-ray tile of a group in a fixed tree order into partials[group][tile];
+// pass 2 sums a group's partials in a fixed order.  Stats: n, Sx, Sy, Sz, Sxx, Syy, Sxy.
+constexpr int kStats = 7;
+struct SpotArgs {
+    const void* __restrict__ plane;
+    double* __restrict__ partials;
+    double* __restrict__ stats;
+    int64_t gsize, ngroups, tiles;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void spot_partial_kernel(SpotArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.y, tile = blockIdx.x;
+    const int64_t j = tile * kBlock + threadIdx.x;
+    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+    if (j < a.gsize) {
+        const T* r = static_cast<const T*>(a.plane) + (g * a.gsize + j) * 8;
+        const double x = r[0], y = r[1], z = r[2];
+        if (x - x == 0.0 && y - y == 0.0) {
+            v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
+        }
+    }
+    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(kBlock) void spot_final_kernel(SpotArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.x;
+    double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+    for (int64_t t = threadIdx.x; t < a.tiles; t += kBlock)
+        for (int k = 0; k < kStats; ++k) v[k] += a.partials[(g * a.tiles + t) * kStats + k];
+    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = kBlock / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < kStats) a.stats[g * kStats + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// Spot-diagram sweep, fused (C5).  Group g is the fan get_ray_fan(pt_g, ..., wl_g)
+// (RT:45-96, same per-ray arithmetic as ray_fan_kernel, angles from the caller's tables); each ray is
+// generated in registers, traced through the plan keeping only its final state, and reduced into the
+// same 256-ray tile partials as spot_partial_kernel.  spot_final_kernel then produces statistics
+// bit-identical to generating, tracing (planes='final') and reducing separately -- without the
+// 3 x 64 B per ray of HBM traffic and the launches in between.
+struct SweepArgs {
+    const DevSurface<double>* __restrict__ surf;
+    const DevMaterial<double>* __restrict__ mats;
+    const double* __restrict__ table;
+    const double2* __restrict__ tab;    // (cos, sin): thetas [n_thetas], then phis [nphis]
+    const double* __restrict__ grp;     // per group: x, y, z, wavelength
+    double* __restrict__ partials;
+    int64_t n_thetas, nphis, gsize, tiles;
+    double c[3], ex[3], ey[3];
+    int32_t nsurf;
+};
+
+template <typename TS>
+__device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
+
+// Two rays per lane: block b covers tiles 2b and 2b+1 of its group; both rays go through each surface
+// in one straight-line region (propagate_surface_pair) so two independent dependency chains
+// interleave (-6 % vs one ray per lane); each tile is reduced separately, with the same tree as
+// spot_partial_kernel.
+template <typename TS, int FEAT>
+__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+    __shared__ double red[kStats][kBlock];
+    const int64_t g = blockIdx.y;
+    const int64_t tileA = 2 * int64_t(blockIdx.x), tileB = tileA + 1;
+    const int64_t jA = tileA * kBlock + threadIdx.x, jB = tileB * kBlock + threadIdx.x;
+    const bool okA = jA < a.gsize, okB = jB < a.gsize;
+    const double* gp = a.grp + 4 * g;
+    auto gen = [&](int64_t j) {
+        const int64_t jj = j < a.gsize ? j : 0;
+        const int64_t it = jj % a.n_thetas, ip = jj / a.n_thetas;
+        const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
+        const double ct = t.x, st = t.y, cp = ph.x, sp = ph.y;
+        Ray<double> r;
+        r.x = stored<TS>(gp[0]); r.y = stored<TS>(gp[1]); r.z = stored<TS>(gp[2]);
+        r.dx = stored<TS>(a.c[0] * ct + a.ex[0] * cp * st + a.ey[0] * sp * st);
+        r.dy = stored<TS>(a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st);
+        r.dz = stored<TS>(a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st);
+        r.ph = 0.0;
+        r.wl = stored<TS>(gp[3]);
+        return r;
+    };
+    Ray<double> rA = gen(jA), rB = gen(jB);
+    const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
+    const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
+    const cptr<double> table = (cptr<double>)(a.table);
+    const double wl0 = rA.wl;                          // one wavelength per group
+    double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
+    for (int s = 0; s < a.nsurf; ++s) {
+        const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
+        const DevSurface<double> sd = load_surface<double>(surf + s);
+        Ray<double> aA, aB;
+        propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, aA, aB);
+        rA = aA;
+        rB = aB;
+        n_cur = n_next;
+    }
+    auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
+        double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
+        if (ok) {
+            const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
+            if (x - x == 0.0 && y - y == 0.0) {
+                v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
+            }
+        }
+        for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
+        __syncthreads();
+        for (int w = kBlock / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w)
+                for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x < kStats && tile < a.tiles)
+            a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
+        __syncthreads();
+    };
+    reduce(rA, okA, tileA);
+    reduce(rB, okB, tileB);
+}
+
+// griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
+__global__ __launch_bounds__(kBlock) void grid_interp_kernel(rtpb_triangulation t, const double* __restrict__ xs,
+                                                             int64_t nx, const double* __restrict__ ys, int64_t ny,
+                                                             double radius, double* __restrict__ phase_out,
+                                                             double* __restrict__ field_out) {
+    const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (k >= nx * ny) return;
+    const int64_t iy = k / nx, ix = k % nx;
+    const double x = xs[ix], y = ys[iy];
+    constexpr double eps = 100.0 * 2.220446049250313e-16;      // scipy qhull: 100 * DBL_EPSILON
+    double phase = __builtin_nan("");
+    const double fx = (x - t.x0) / t.cell_w, fy = (y - t.y0) / t.cell_h;
+    if (fx >= 0.0 && fy >= 0.0 && fx < double(t.cells_x) && fy < double(t.cells_y)) {
+        const int64_t cell = int64_t(fy) * t.cells_x + int64_t(fx);
+        for (int32_t q = t.cell_start[cell]; q < t.cell_start[cell + 1]; ++q) {
+            const int32_t s = t.cell_tris[q];
+            const double* T = t.transform + 6 * int64_t(s);
+            // scipy/spatial/_qhull.pyx _barycentric_inside / _barycentric_coordinates (ndim = 2)
+            double c0 = 0.0;
+            c0 += T[0] * (x - T[4]);
+            c0 += T[1] * (y - T[5]);
+            double c1 = 0.0;
+            c1 += T[2] * (x - T[4]);
+            c1 += T[3] * (y - T[5]);
+            const double c2 = (1.0 - c0) - c1;
+            if (!(-eps <= c0 && c0 <= 1.0 + eps) || !(-eps <= c1 && c1 <= 1.0 + eps) ||
+                !(-eps <= c2 && c2 <= 1.0 + eps))
+                continue;
+            // scipy/interpolate/_interpnd.pyx LinearNDInterpolator._do_evaluate
+            const int32_t* v = t.simplices + 3 * int64_t(s);
+            double o = 0.0;
+            o = o + c0 * t.values[v[0]];
+            o = o + c1 * t.values[v[1]];
+            o = o + c2 * t.values[v[2]];
+            phase = o;
+            break;
+        }
+    }
+    if (phase_out) phase_out[k] = phase;
+    if (field_out) {
+        const bool off = sqrt(x * x + y * y) > radius || phase != phase;
+        field_out[2 * k] = off ? 0.0 : cos(phase);
+        field_out[2 * k + 1] = off ? 0.0 : sin(phase);
+    }
+}
+
+
+}  // namespace
+
+extern "C" {
+
+int rtpb_intersect_rays(int32_t device, int32_t dtype, const void* ray1, int64_t n1, const void* ray2, int64_t n2,
+                        void* pts_out, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    if (n1 < 0 || n2 < 0 || (n1 != n2 && n1 != 1 && n2 != 1))
+        return fail(RTPB_E_INVALID, "ray1 and ray2 must be the same length");
+    const int64_t n = std::max(n1, n2);
+    if (n == 0) return RTPB_OK;
+    if (!ray1 || !ray2 || !pts_out) return fail(RTPB_E_INVALID, "NULL pointer");
+    IsectArgs a{ray1, ray2, pts_out, n, n1, n2};
+    DeviceGuard g(device);
+    const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+    if (dtype == RTPB_F64)
+        hipLaunchKernelGGL(intersect_kernel<double>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(intersect_kernel<float>, dim3(blocks), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t group_size, int64_t n_groups,
+                    double* workspace, int64_t workspace_len, double* stats_out, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (dtype != RTPB_F64 && dtype != RTPB_F32) return fail(RTPB_E_INVALID, "bad dtype");
+    if (group_size <= 0 || n_groups <= 0 || !plane || !stats_out || !workspace)
+        return fail(RTPB_E_INVALID, "bad spot-stats arguments");
+    const int64_t tiles = (group_size + kBlock - 1) / kBlock;
+    if (workspace_len < n_groups * tiles * kStats)
+        return fail(RTPB_E_INVALID, "workspace too small: need n_groups * ceil(group_size/256) * 7 doubles");
+    if (tiles > 65535 * 16384ll || n_groups > 65535) return fail(RTPB_E_LIMIT, "too many groups");
+    SpotArgs a{plane, workspace, stats_out, group_size, n_groups, tiles};
+    DeviceGuard g(device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(n_groups));
+    if (dtype == RTPB_F64) hipLaunchKernelGGL(spot_partial_kernel<double>, grid, dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(spot_partial_kernel<float>, grid, dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, const double* group_params,
+                    int64_t n_thetas, int64_t nphis, const double center_ray[3], const double ex[3],
+                    const double ey[3], const double* theta_cos_sin, const double* phi_cos_sin, double* workspace,
+                    int64_t workspace_len, double* stats_out, void* stream) {
+    auto* plan = const_cast<rtpb_plan*>(plan_c);
+    if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n_groups <= 0 || n_thetas <= 0 || nphis <= 0 || !group_params || !center_ray || !ex || !ey ||
+        !theta_cos_sin || !phi_cos_sin || !workspace || !stats_out)
+        return fail(RTPB_E_INVALID, "bad spot-sweep arguments");
+    const int64_t gsize = n_thetas * nphis;
+    const int64_t tiles = (gsize + kBlock - 1) / kBlock;
+    if (workspace_len < n_groups * tiles * kStats)
+        return fail(RTPB_E_INVALID, "workspace too small: need n_groups * ceil(n_thetas*nphis/256) * 7 doubles");
+    if (tiles > 0x7fffffffll || n_groups > 65535) return fail(RTPB_E_LIMIT, "too many groups or rays per group");
+    DeviceGuard g(device);
+    void* blob = nullptr;
+    rc = plan_device_blob(plan, device, &blob);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // one upload: trig tables then the per-group parameters
+    const size_t ntab = size_t(n_thetas + nphis), bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double);
+    void* dbuf = nullptr;
+    HIP_TRY(hipMallocAsync(&dbuf, bytes, st));
+    PinnedStaging& g_pinned = pinned_staging();
+    rc = g_pinned.reserve(bytes);
+    if (rc) return rc;
+    std::memcpy(g_pinned.buf, theta_cos_sin, size_t(2 * n_thetas) * sizeof(double));
+    std::memcpy(g_pinned.buf + 2 * n_thetas, phi_cos_sin, size_t(2 * nphis) * sizeof(double));
+    std::memcpy(g_pinned.buf + 2 * ntab, group_params, size_t(4 * n_groups) * sizeof(double));
+    rc = g_pinned.upload(dbuf, bytes, st);
+    if (rc) return rc;
+    SweepArgs a{};
+    a.surf = static_cast<const DevSurface<double>*>(blob);
+    a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
+    a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
+    a.tab = static_cast<const double2*>(dbuf);
+    a.grp = reinterpret_cast<const double*>(static_cast<char*>(dbuf) + ntab * sizeof(double2));
+    a.partials = workspace;
+    a.n_thetas = n_thetas;
+    a.nphis = nphis;
+    a.gsize = gsize;
+    a.tiles = tiles;
+    for (int j = 0; j < 3; ++j) {
+        a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
+    }
+    a.nsurf = plan->nsurf;
+    const dim3 grid(static_cast<unsigned>((tiles + 1) / 2), static_cast<unsigned>(n_groups));
+    auto go = [&](auto tag) {
+        using TS = decltype(tag);
+        if (plan->feat == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
+        else if (plan->feat == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((sweep_kernel<TS, 3>), grid, dim3(kBlock), 0, st, a);
+    };
+    if (plan->dtype == RTPB_F64) go(double{});
+    else go(float{});
+    HIP_TRY(hipGetLastError());
+    SpotArgs sa{nullptr, workspace, stats_out, gsize, n_groups, tiles};
+    hipLaunchKernelGGL(spot_final_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(kBlock), 0, st, sa);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(dbuf, st));
+    return RTPB_OK;
+}
+
+int rtpb_grid_interpolate(int32_t device, const rtpb_triangulation* tri, const double* xs, int64_t nx,
+                          const double* ys, int64_t ny, double radius, double* phase_out, double* field_out,
+                          void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (!tri || !xs || !ys || nx <= 0 || ny <= 0) return fail(RTPB_E_INVALID, "bad grid-interpolate arguments");
+    if (tri->n_tri < 0 || (tri->n_tri > 0 && (!tri->transform || !tri->simplices || !tri->values)) ||
+        tri->cells_x <= 0 || tri->cells_y <= 0 || !tri->cell_start || !tri->cell_tris || !(tri->cell_w > 0.0) ||
+        !(tri->cell_h > 0.0))
+        return fail(RTPB_E_INVALID, "bad triangulation descriptor");
+    if (!phase_out && !field_out) return RTPB_OK;
+    DeviceGuard g(device);
+    const int64_t total = nx * ny;
+    hipLaunchKernelGGL(grid_interp_kernel, dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, static_cast<hipStream_t>(stream), *tri, xs, nx, ys, ny, radius, phase_out, field_out);
+    HIP_TRY(hipGetLastError());
+    return RTPB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+// rtpb_internal.h -- internals shared by the translation units of librtpb.so (not part of the ABI):
+// launch constants, error plumbing, the plan object, descriptor access through the constant address
+// space, ray record loads/stores and the per-wave LDS tiles that turn 64-byte AoS records into 1 KiB
+// contiguous stores.  The public interface is include/rtpb.h; the per-ray arithmetic is rtpb_math.h.
+//
+// Translation units:
+//   rtpb_core.hip          errors, plans (lowering to device blobs), device queries
+//   rtpb_trace.hip         the fused trace kernel, rtpb_trace / rtpb_trace_host, tuning and timing
+//   rtpb_generators.hip    device ray fans and collimated bundles (RT:45-161)
+//   rtpb_analysis.hip      intersect_rays, spot statistics, the fused spot sweep, grid interpolation
+//   rtpb_surface_ops.hip   propagate_ray2plane and the user-geometry hook kernels
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rtpb.h"
+#include "rtpb_math.h"
+
+namespace rtpbi {
+
+using namespace rtpb;
+
+constexpr int kBlock = 256;               // auxiliary kernels
+// The trace kernel runs one wave per workgroup: a workgroup's LDS tile and wave slot are released the
+// moment its wave finishes, so the dispatcher refills CUs wave by wave instead of waiting for the
+// slowest of four (-6 % kernel time on C2 f64 full history vs 256-thread workgroups, same occupancy).
+#if defined(RTPB_EXP_TRACE_BLOCK)          // experiment builds only (tools/ab_libs.py)
+constexpr int kTraceBlock = RTPB_EXP_TRACE_BLOCK;
+#else
+constexpr int kTraceBlock = 64;
+#endif
+constexpr int kMaxDevices = 64;
+
+// Thread-local message of the last failure (rtpb_last_error) and the helper every entry point uses.
+extern thread_local std::string g_last_error;
+int fail(int code, const std::string& msg);
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RTPB_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_));          \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// ---------------------------------------------------------------------------------- kernel args
+template <typename TS>
+struct TraceArgs {
+    const TS* __restrict__ in;
+    TS* __restrict__ out;
+    const DevSurface<double>* __restrict__ surf;
+    const DevMaterial<double>* __restrict__ mats;
+    const double* __restrict__ table;
+    int64_t n;
+    int64_t in_fs;        // SOA input field stride
+    int64_t out_ps;       // output plane (slot) stride
+    int64_t out_fs;       // SOA output field stride
+    uint64_t mask_lo;
+    uint64_t mask_hi;
+    int32_t nsurf;
+};
+
+// Descriptors are read-only for the whole launch: read them through the constant address space so
+// the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.
+template <typename T> using cptr = const __attribute__((address_space(4))) T*;
+
+template <typename T>
+__device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
+    DevSurface<T> d;
+    d.kind = p->kind;
+    d.pad = 0;
+    for (int j = 0; j < 3; ++j) {
+        d.c[j] = p->c[j];
+        d.nrm[j] = p->nrm[j];
+        d.ax[j] = p->ax[j];
+    }
+    d.R = p->R; d.R2 = p->R2; d.absR = p->absR; d.ap = p->ap; d.f = p->f; d.sin_a = p->sin_a; d.tol = p->tol;
+    d.ap_sq = p->ap_sq; d.shell_lo = p->shell_lo; d.shell_hi = p->shell_hi;
+    return d;
+}
+
+template <typename T>
+__device__ __forceinline__ DevMaterial<T> load_material(cptr<DevMaterial<T>> p) {
+    DevMaterial<T> d;
+    d.kind = p->kind;
+    d.table_off = p->table_off;
+    d.table_len = p->table_len;
+    d.pad = 0;
+    for (int j = 0; j < 6; ++j) d.c[j] = p->c[j];
+    return d;
+}
+
+template <typename TS, int LAYOUT>
+__device__ __forceinline__ Ray<double> load_ray(const TS* __restrict__ in, int64_t i, int64_t fs) {
+    Ray<double> r;
+    if constexpr (LAYOUT == RTPB_AOS) {
+        if constexpr (sizeof(TS) == 8) {
+            const double2* p = reinterpret_cast<const double2*>(in + i * 8);
+            const double2 a = p[0], b = p[1], c = p[2], d = p[3];
+            r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
+        } else {
+            const float4* p = reinterpret_cast<const float4*>(in + i * 8);
+            const float4 a = p[0], b = p[1];
+            r.x = a.x; r.y = a.y; r.z = a.z; r.dx = a.w; r.dy = b.x; r.dz = b.y; r.ph = b.z; r.wl = b.w;
+        }
+    } else {
+        r.x = in[i]; r.y = in[fs + i]; r.z = in[2 * fs + i]; r.dx = in[3 * fs + i];
+        r.dy = in[4 * fs + i]; r.dz = in[5 * fs + i]; r.ph = in[6 * fs + i]; r.wl = in[7 * fs + i];
+    }
+    return r;
+}
+
+template <typename TS, int LAYOUT>
+__device__ __forceinline__ void store_ray(TS* __restrict__ out, int64_t i, int64_t fs, const Ray<double>& r) {
+    if constexpr (LAYOUT == RTPB_AOS) {
+        if constexpr (sizeof(TS) == 8) {
+            double2* p = reinterpret_cast<double2*>(out + i * 8);
+            p[0] = make_double2(r.x, r.y);
+            p[1] = make_double2(r.z, r.dx);
+            p[2] = make_double2(r.dy, r.dz);
+            p[3] = make_double2(r.ph, r.wl);
+        } else {
+            float4* p = reinterpret_cast<float4*>(out + i * 8);
+            p[0] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
+            p[1] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
+        }
+    } else {
+        out[i] = TS(r.x); out[fs + i] = TS(r.y); out[2 * fs + i] = TS(r.z); out[3 * fs + i] = TS(r.dx);
+        out[4 * fs + i] = TS(r.dy); out[5 * fs + i] = TS(r.dz); out[6 * fs + i] = TS(r.ph); out[7 * fs + i] = TS(r.wl);
+    }
+}
+
+__device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
+    return p < 64 ? ((lo >> p) & 1ull) : ((hi >> (p - 64)) & 1ull);
+}
+
+// ---------------------------------------------------------------------------------- AOS plane stores
+// A ray record is 8*sizeof(TS) = 64 B (f64) or 32 B (f32).  Stored directly, lane l writes its record
+// with 16-byte stores at a 64/32-byte lane stride: every store instruction touches 4 KiB of address
+// space at 25/50 % density and the history write (11 of 12 bytes moved) runs at ~3.4 TB/s.  Staged,
+// each wave first drops its 64 records into a private LDS tile, then lane l stores 16-byte chunks
+// l, l+64, ... of the wave's contiguous 4/2 KiB block: every global store instruction writes 1 KiB
+// contiguous.  The tile is XOR-swizzled so the b128 writes and reads are bank-conflict free:
+//   f64: chunk p of ray L lives at slot 4L + (p ^ ((L >> 1) & 3));  f32: 2L + (p ^ ((L >> 2) & 1)).
+// Only the owning wave touches its tile and LDS executes one wave's DS operations in order, so no
+// workgroup barrier is needed -- just the lgkmcnt waits (asm, with a memory clobber so the compiler
+// cannot move the tile accesses across them).
+constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void gstore(double2* p, const double2& v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void gstore(float4* p, const float4& v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
+    else *p = v;
+}
+
+// Stage one record into the wave's tile (XOR-swizzled slots)
+template <typename TS>
+__device__ __forceinline__ void tile_write(uint4* __restrict__ tile, int lane, const Ray<double>& r) {
+    if constexpr (sizeof(TS) == 8) {
+        const int sw = (lane >> 1) & 3;
+        double2* t = reinterpret_cast<double2*>(tile);
+        t[4 * lane + (0 ^ sw)] = make_double2(r.x, r.y);
+        t[4 * lane + (1 ^ sw)] = make_double2(r.z, r.dx);
+        t[4 * lane + (2 ^ sw)] = make_double2(r.dy, r.dz);
+        t[4 * lane + (3 ^ sw)] = make_double2(r.ph, r.wl);
+    } else {
+        const int sw = (lane >> 2) & 1;
+        float4* t = reinterpret_cast<float4*>(tile);
+        t[2 * lane + (0 ^ sw)] = make_float4(float(r.x), float(r.y), float(r.z), float(r.dx));
+        t[2 * lane + (1 ^ sw)] = make_float4(float(r.dy), float(r.dz), float(r.ph), float(r.wl));
+    }
+}
+
+// Write the wave's staged block (64 records) to `plane` lane-contiguously: 1 KiB per store instruction.
+// Callers wait for the tile writes first (lgkmcnt(0)); the compiler waits for the tile reads before the
+// global stores that consume them, and a wave's DS operations execute in order, so the next tile_write
+// cannot overtake these reads.
+template <typename TS, bool NT>
+__device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
+                                           int64_t n, int lane) {
+    if constexpr (sizeof(TS) == 8) {
+        const double2* t = reinterpret_cast<const double2*>(tile);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
+        double2* g = reinterpret_cast<double2*>(plane + ray0 * 8);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
+            const double2 v = t[4 * rr + (pp ^ ((rr >> 1) & 3))];
+            if (c < nchunks) gstore(g + c, v, NT);
+        }
+    } else {
+        const float4* t = reinterpret_cast<const float4*>(tile);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
+        float4* g = reinterpret_cast<float4*>(plane + ray0 * 8);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
+            const float4 v = t[2 * rr + (pp ^ ((rr >> 2) & 1))];
+            if (c < nchunks) gstore(g + c, v, NT);
+        }
+    }
+}
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Inverse of tile_flush for the input: lane l loads 16-byte chunks l, l+64, ... of the wave's contiguous
+// record block (1 KiB per load instruction) into the tile, then reads back its own record.
+template <typename TS>
+__device__ __forceinline__ Ray<double> tile_load(uint4* __restrict__ tile, const TS* __restrict__ in, int64_t ray0,
+                                                 int64_t n, int lane) {
+    Ray<double> r;
+    if constexpr (sizeof(TS) == 8) {
+        double2* t = reinterpret_cast<double2*>(tile);
+        const double2* g = reinterpret_cast<const double2*>(in + ray0 * 8);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
+            const double2 v = g[c < nchunks ? c : nchunks - 4 + pp];      // tail lanes re-read the last ray
+            t[4 * rr + (pp ^ ((rr >> 1) & 3))] = v;
+        }
+        lds_wait();
+        const int sw = (lane >> 1) & 3;
+        const double2 a = t[4 * lane + (0 ^ sw)], b = t[4 * lane + (1 ^ sw)], c = t[4 * lane + (2 ^ sw)],
+                      d = t[4 * lane + (3 ^ sw)];
+        r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
+    } else {
+        float4* t = reinterpret_cast<float4*>(tile);
+        const float4* g = reinterpret_cast<const float4*>(in + ray0 * 8);
+        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
+            const float4 v = g[c < nchunks ? c : nchunks - 2 + pp];
+            t[2 * rr + (pp ^ ((rr >> 2) & 1))] = v;
+        }
+        lds_wait();
+        const int sw = (lane >> 2) & 1;
+        const float4 a = t[2 * lane + (0 ^ sw)], b = t[2 * lane + (1 ^ sw)];
+        r.x = a.x; r.y = a.y; r.z = a.z; r.dx = a.w; r.dy = b.x; r.dz = b.y; r.ph = b.z; r.wl = b.w;
+    }
+    return r;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Per-thread pinned staging buffer for small host->device uploads (tables, per-group parameters): the
+// caller fills it, then upload() copies it to `dev` on `st`.  It is reused once its previous copy has
+// completed, so uploads never synchronise the stream.
+struct PinnedStaging {
+    double* buf = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+
+    int reserve(size_t bytes) {
+        if (done) HIP_TRY(hipEventSynchronize(done));
+        if (!done) HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        if (cap < bytes) {
+            if (buf) HIP_TRY(hipHostFree(buf));
+            buf = nullptr;
+            cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&buf), bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return RTPB_OK;
+    }
+    int upload(void* dev, size_t bytes, hipStream_t st) {
+        HIP_TRY(hipMemcpyAsync(dev, buf, bytes, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(done, st));
+        return RTPB_OK;
+    }
+};
+PinnedStaging& pinned_staging();     // this thread's buffer
+
+}  // namespace rtpbi
+
+// ---------------------------------------------------------------------------------- plans
+struct rtpb_plan {
+    int32_t dtype = RTPB_F64;
+    int32_t nsurf = 0;
+    std::vector<rtpb_surface> surf;
+    std::vector<rtpb_material> mats;    // table pointers cleared; see table_off/table_len
+    std::vector<int32_t> table_off;
+    std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
+    int feat = 0;                       // kernel features needed: 1 = PerfectLens, 2 = POLY6 material
+    std::mutex mu;
+    void* blob[rtpbi::kMaxDevices] = {};
+    size_t off_mats = 0, off_table = 0, blob_bytes = 0;   // blob layout, fixed at plan creation
+};
+
+namespace rtpbi {
+// Device copy of a plan's descriptors (created on first use per device, then immutable).
+int plan_device_blob(rtpb_plan* p, int dev, void** out);
+// RTPB_OK, or RTPB_E_NODEV with the message set.
+int check_device(int dev);
+}  // namespace rtpbi

@@ -1,5 +1,5 @@
 // rtpb_math.h -- per-ray arithmetic of the sequential ray trace, shared by the gfx950 kernel
-// (rtpb_device.hip) and the CPU test harness (tests/native/math_harness.cpp).
+// (rtpb_trace.hip and the other kernels) and the CPU test harness (tests/native/math_harness.cpp).
 //
 // Every function restates one piece of the reference (QI2lab/ray_trace_pb @ 2024_10_08,
 // src/raytrace/raytrace.py = RT, src/raytrace/materials.py = MAT) for ONE ray, with the operations

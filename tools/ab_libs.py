@@ -1,7 +1,10 @@
 """A/B several builds of librtpb.so in ONE process (interleaved, randomised order, median of rounds).
 
-Each extra library is an experiment build of the same sources (e.g. `-DRTPB_EXP_NO_ONSURFACE`, which
-drops work and is NOT bit-exact) -- used only to find where kernel time goes, never shipped.
+Each extra library is an experiment build of the same sources, e.g.
+    python -c "from ray_trace_pb_amd import _build; _build.build(extra_flags=['-DRTPB_EXP_NO_ONSURFACE'],
+               out='ray_trace_pb_amd/exp_noons.so')"
+(`-DRTPB_EXP_NO_ONSURFACE` drops work and is NOT bit-exact) -- used only to find where kernel time goes,
+never shipped.
 
     python tools/ab_libs.py ray_trace_pb_amd/exp_X.so ... [--rays N] [--configs c2,c5]
 """
