@@ -258,7 +258,8 @@ int rtpb_grid_interpolate(int32_t device, const rtpb_triangulation* tri, const d
    "stage_input": 1 = also load AOS input records through the LDS tile (1 KiB per load instruction);
    0 (default) = 4 x 16-byte loads per lane.
    "waves_per_eu": 0 (default: compiler choice, 4 waves/SIMD) or 5 = occupancy target for the
-   AOS->AOS staged kernel (the compiler then spills to scratch to fit). */
+   AOS->AOS staged kernel (the compiler then spills to scratch to fit).
+   "host_chunk_mib": input + output bytes per pipelined chunk of rtpb_trace_host (default 128). */
 int rtpb_set_tuning(const char* key, int64_t value);
 
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */

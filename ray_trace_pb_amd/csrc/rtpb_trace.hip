@@ -152,6 +152,7 @@ std::atomic<int> g_aos_staging{1};
 std::atomic<int> g_nt_stores{1};
 std::atomic<int> g_waves_per_eu{0};
 std::atomic<int> g_stage_input{0};
+std::atomic<int> g_host_chunk_mib{128};
 
 template <typename T, int IL, int OL, int ST, int W, int FEAT>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
@@ -320,7 +321,9 @@ int host_shard_pipeline(rtpb_plan* plan, int dev, const char* in, char* out, int
     // pinned (page-locked, e.g. torch pin_memory) output: DMA every plane slice straight into place
     const bool direct = is_pinned_host(out) && is_pinned_host(out + (int64_t(nslots) * n_rays * rec - 1));
     // ~128 MiB of output per chunk (at least 64k rays), two chunks in flight
-    const int64_t chunk = std::min<int64_t>(b - a, std::max<int64_t>(1 << 16, (int64_t(128) << 20) / int64_t(nslots * rec)));
+    // chunk: ~g_host_chunk_mib of input + output per chunk (at least 64k rays), two chunks in flight
+    const int64_t target = int64_t(g_host_chunk_mib.load()) << 20;
+    const int64_t chunk = std::min<int64_t>(b - a, std::max<int64_t>(1 << 16, target / int64_t((nslots + 1) * rec)));
     int rc = stage_reserve(hs, chunk * rec, chunk * rec * nslots);
     if (rc) return rc;
     const int64_t nchunks = (b - a + chunk - 1) / chunk;
@@ -337,7 +340,7 @@ int host_shard_pipeline(rtpb_plan* plan, int dev, const char* in, char* out, int
         const int buf = static_cast<int>(k & 1);
         const int64_t c0 = a + k * chunk, m = std::min<int64_t>(chunk, b - c0);
         // pin_in[buf] / pin_out[buf] were last used by chunk k-2, whose event was waited in scatter(k-2)
-        std::memcpy(hs.pin_in[buf], in + c0 * rec, static_cast<size_t>(m * rec));
+        parallel_scatter(static_cast<char*>(hs.pin_in[buf]), in + c0 * rec, 1, 0, static_cast<int64_t>(m * rec), T);
         HIP_TRY(hipMemcpyAsync(hs.d_in[buf], hs.pin_in[buf], m * rec, hipMemcpyHostToDevice, hs.st));
         rc = trace_impl(plan, dev, hs.d_in[buf], m, RTPB_AOS, 0, hs.d_out[buf], RTPB_AOS, m * 8, 0, lo, hi, hs.st);
         if (rc) return rc;
@@ -467,6 +470,11 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     }
     if (std::strcmp(key, "stage_input") == 0) {
         g_stage_input.store(value != 0);
+        return RTPB_OK;
+    }
+    if (std::strcmp(key, "host_chunk_mib") == 0) {
+        if (value < 1 || value > 4096) return fail(RTPB_E_INVALID, "host_chunk_mib must be in [1, 4096]");
+        g_host_chunk_mib.store(static_cast<int>(value));
         return RTPB_OK;
     }
     if (std::strcmp(key, "waves_per_eu") == 0) {

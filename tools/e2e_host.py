@@ -19,13 +19,13 @@ V = mat.Vacuum()
 out = system.ray_trace(rays, V, V)            # warm (plan, allocations)
 for planes in ("all", "final"):
     ts = []
-    for _ in range(5):
+    for _ in range(15):
         t0 = time.perf_counter()
         out = system.ray_trace(rays, V, V, planes=planes)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    print(f"numpy e2e planes={planes}: {t * 1e3:.1f} ms  -> {n * 5 / t:.3g} ray-surf/s, "
-          f"host bytes {(rays.nbytes + out.nbytes) / t / 1e9:.1f} GB/s")
+    print(f"numpy e2e planes={planes}: median {t * 1e3:.1f} ms (min {min(ts) * 1e3:.1f}) -> {n * 5 / t:.3g} "
+          f"ray-surf/s, host bytes {(rays.nbytes + out.nbytes) / t / 1e9:.1f} GB/s")
 dev = torch.device("cuda:0")
 buf = torch.empty(88_000_000, dtype=torch.float64, device=dev)
 src = torch.empty(96_000_000, dtype=torch.float64, device=dev)
