@@ -121,7 +121,13 @@ void trace_kernel(TraceArgs<TS> a) {
             }
         };
         Ray<T> after;
+#if defined(RTPB_EXP_NO_COMPUTE)           // experiment only: the kernel's pure memory path
+        after = r;
+        after.ph = r.ph + n_next + n_cur;
+        emit_at(r);
+#else
         propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, emit_at, after);
+#endif
         if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
             if (st_after) tile_write<TS>(tile_b, lane, after);
