@@ -450,3 +450,34 @@ def test_more_than_2_31_rays_in_one_launch():
     ref = oracle(system, m0, m1, r_in)[-1].astype(np.float32)
     assert np.array_equal(got, ref, equal_nan=True)
     assert np.isfinite(got[:, 0]).sum() > 1000        # not an all-NaN comparison
+
+
+def test_concurrent_host_threads_give_identical_results():
+    """Several Python threads tracing different systems at once (NumPy and torch paths, shared plan
+    cache, one device): every result equals its single-threaded trace."""
+    import threading
+    cases = ["c1_plano_convex", "c2_achromat", "c4_mirror", "stress"]
+    built = [build_case(c) for c in cases]
+    want = [b[4] for b in built]
+    got = [[None] * 3 for _ in cases]
+    errors = []
+
+    def work(k):
+        try:
+            system, m0, m1, rays, _ = built[k]
+            for it in range(3):
+                if it % 2:
+                    got[k][it] = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1).cpu().numpy()
+                else:
+                    got[k][it] = system.ray_trace(rays, m0, m1)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(cases))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for k in range(len(cases)):
+        for it in range(3):
+            assert np.array_equal(got[k][it], want[k], equal_nan=True), (cases[k], it)
