@@ -481,3 +481,39 @@ def test_concurrent_host_threads_give_identical_results():
     for k in range(len(cases)):
         for it in range(3):
             assert np.array_equal(got[k][it], want[k], equal_nan=True), (cases[k], it)
+
+
+def test_snell_and_reflection_invariants_at_full_size():
+    """SURVEY §4 property tests on 1M-ray bundles: at every refracting sphere of C2,
+    n1 |d_in x N| = n2 |d_out x N| and d_in, N, d_out are coplanar; at the C4 mirror the normal
+    component flips and the tangential one is kept (angle in = angle out)."""
+    system = systems.c2_system(rt, mat)
+    rays = systems.c2_rays(1_000_000)
+    h = system.ray_trace(torch.from_numpy(rays).to(DEV), mat.Vacuum(), mat.Vacuum()).cpu().numpy()
+    mats = [mat.Vacuum()] + list(system.materials) + [mat.Vacuum()]
+    wl = rays[:, 7]
+    checked = 0
+    for i, s in enumerate(system.surfaces):
+        if type(s) is not rt.SphericalSurface:
+            continue
+        at, after, before = h[2 * i + 1], h[2 * i + 2], h[2 * i]
+        live = ~np.isnan(after).any(axis=1)
+        N = (at[live, :3] - s.center) / s.radius
+        d1, d2 = before[live, 3:6], after[live, 3:6]
+        n1, n2 = mats[i].n(wl[live]), mats[i + 1].n(wl[live])
+        s1 = np.linalg.norm(np.cross(d1, N), axis=1)
+        s2 = np.linalg.norm(np.cross(d2, N), axis=1)
+        np.testing.assert_allclose(n1 * s1, n2 * s2, rtol=0, atol=1e-12)
+        assert np.max(np.abs(np.sum(np.cross(d1, N) * d2, axis=1))) < 1e-12
+        checked += live.sum()
+    assert checked > 2_000_000
+    # mirror: a tilted PlaneMirror hit by a 1M-ray fan
+    mirror = rt.System([rt.PlaneMirror([0, 0, 10], systems.unit([0.0, 0.3, -1.0]), 50)], [])
+    fan = rt.get_ray_fan([0, 0, 0], 0.2, 1001, 0.5, nphis=1000, device=DEV)
+    hm = mirror.ray_trace(fan, mat.Vacuum(), mat.Vacuum()).cpu().numpy()
+    live = ~np.isnan(hm[2]).any(axis=1)
+    assert live.mean() > 0.99
+    N = systems.unit([0.0, 0.3, -1.0])
+    din, dout = hm[0, live, 3:6], hm[2, live, 3:6]
+    np.testing.assert_allclose(dout @ N, -(din @ N), rtol=0, atol=1e-14)
+    np.testing.assert_allclose(dout - (dout @ N)[:, None] * N, din - (din @ N)[:, None] * N, rtol=0, atol=1e-14)
