@@ -234,10 +234,13 @@ def main():
         step()
     ev1.record()
     torch.cuda.synchronize()
+    # each rank's own clock stops at its device sync; the job time is the max over ranks (all_reduce
+    # below), so the closing barrier's own latency (gloo over loopback, ~0.1-0.5 ms) is not charged
+    # to the K steps -- it would dominate at the driver's small K
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
