@@ -2,7 +2,7 @@
 
 Run from anywhere inside this container (not on the GPU box -- /root/reference does not exist there):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [name,...]     # only the named recipes (no paraxial/generator files)
 
 The script re-launches itself in a child interpreter whose ``sys.path`` holds only
 /root/reference/src (the reference's ``raytrace`` package) and this directory, with cwd=/tmp, so the
@@ -33,7 +33,10 @@ def _child():
     warnings.simplefilter("ignore")
     meta = {"numpy": np.__version__, "reference": "QI2lab/ray_trace_pb @ 2024_10_08"}
 
+    only = [v for v in os.environ.get("RTPB_GOLDEN_ONLY", "").split(",") if v]
     for name, recipe in systems.RECIPES.items():
+        if only and name not in only:
+            continue
         system, rays, m_init, m_final = recipe(rt, mat)
         hist = system.ray_trace(rays, m_init, m_final)
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"),
@@ -43,6 +46,8 @@ def _child():
                             meta_json=np.array(json.dumps(meta)))
         print(f"{name:24s} surfaces={len(system.surfaces):2d} rays_in={rays.shape} history={hist.shape} "
               f"nan_rows_final={int(np.isnan(hist[-1]).any(axis=1).sum())}")
+    if only:
+        return
 
     # input-rank cases of System.ray_trace (RT:1175-1178: 1-D -> (1,1,8), 2-D -> (1,N,8), 3-D appended)
     system, rays, m_init, m_final = systems.c1_plano_convex(rt, mat, nrays=5)
@@ -107,5 +112,6 @@ if __name__ == "__main__":
         _child()
     else:
         env = dict(os.environ, PYTHONPATH=f"{REF_SRC}:{HERE}", RTPB_GOLDEN_CHILD="1",
+                   RTPB_GOLDEN_ONLY=sys.argv[1] if len(sys.argv) > 1 else "",
                    MPLBACKEND="Agg", PYTHONDONTWRITEBYTECODE="1")
         sys.exit(subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, cwd="/tmp").returncode)

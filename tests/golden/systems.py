@@ -15,6 +15,8 @@ SURVEY.md §8d) plus edge-case systems written for this repository:
 * C4m plane-mirror system       -- scripts/2021_07_25_mirror.py:9-18
 * C5  ODT excitation path       -- scripts/2021_10_06_ray_trace_system.py:9-145
 * KAT perfect-lens phase        -- scripts/2021_10_28_test_perfect_lens_phase.py:12-38
+* off-axis relay (astigmatism)  -- scripts/2022_08_24_relay_astigmatism.py:9-86
+* lightsheet with ETL           -- scripts/2024_04_01_lightsheet.py:23-133
 
 Ray bundles are built with ``rt.get_ray_fan`` / ``rt.get_collimated_rays`` (reference RT:45-161) or
 with plain NumPy (seeded with ``numpy.random.default_rng``), never with anything module-specific.
@@ -354,6 +356,64 @@ def tir_prism(rt, mat, nrays=400):
     return system, rays, mat.Vacuum(), mat.Vacuum()
 
 
+def astig_relay(rt, mat, nrays=19, offset=5.0):
+    """scripts/2022_08_24_relay_astigmatism.py:9-86: three achromats, the first two displaced off axis
+    by `offset` (the sphere aperture is measured about the ORIGIN-through axis, RT:1527-1535), traced
+    with meridional, sagittal and 100-azimuth collimated bundles at 0.785 um."""
+    wl = 0.785
+    beam_rad = 20e-3 * np.sqrt(1 + (3 / (np.pi * 20e-3 ** 2 / (wl * 1e-3))) ** 2)
+    t100c, r100c, r100i, t100f, r100f, bfl100 = 13.0, 65.8, -56., 2.0, -280.6, 91.5
+    t180c, r180c, r180i, t180f, r180f, bfl180 = 9.5, 144.4, -115.4, 4.0, -328.2, 173.52
+    t300c, r300c, r300i, t300f, bfl300, efl300 = 9.0, 167.7, -285.8, 4.0, 289.81, 300
+    radius = 25.4
+    z180 = 10
+    z100 = (t180c + t180f) + bfl180 + 101.5
+    z300 = z100 + (t100c + t100f) + bfl100 + efl300
+    zend = z300 + (t300c + t300f) + bfl300
+    surfaces = [rt.SphericalSurface(r180c, [offset, 0, z180 + np.abs(r180c)], radius),
+                rt.SphericalSurface(r180i, [offset, 0, z180 + t180c - np.abs(r180i)], radius),
+                rt.SphericalSurface(r180f, [offset, 0, z180 + t180c + t180f - np.abs(r180f)], radius),
+                rt.SphericalSurface(-r100f, [offset, 0, z100 + np.abs(r100f)], radius),
+                rt.SphericalSurface(-r100i, [offset, 0, z100 + t100f + np.abs(r100i)], radius),
+                rt.SphericalSurface(-r100c, [offset, 0, z100 + t100f + t100c - np.abs(r100c)], radius),
+                rt.SphericalSurface.get_on_axis(r300c, z300, radius),
+                rt.SphericalSurface.get_on_axis(r300i, z300 + t300c, radius),
+                rt.FlatSurface([0, 0, z300 + t300c + t300f], [0, 0, 1], radius),
+                rt.FlatSurface([0, 0, zend], [0, 0, 1], radius)]
+    materials = [mat.Nlak22(), mat.Nsf6(), mat.Constant(1), mat.Nsf6ht(), mat.Nlak22(), mat.Constant(1),
+                 mat.Nlak22(), mat.Nsf6(), mat.Constant(1)]
+    rays = np.concatenate((rt.get_collimated_rays([0, 0, 0], beam_rad, nrays, wl),
+                           rt.get_collimated_rays([0, 0, 0], beam_rad, nrays, wl, phi_start=np.pi / 2),
+                           rt.get_collimated_rays([0, 0, 0], beam_rad, nrays, wl, nphis=100)), axis=0)
+    return rt.System(surfaces, materials), rays, mat.Vacuum(), mat.Vacuum()
+
+
+def lightsheet(rt, mat, rad_curv, nrays=1001):
+    """scripts/2024_04_01_lightsheet.py:23-36,72-133: electrically tunable lens (flat + sphere of
+    radius `rad_curv`), two relay PerfectLenses, an objective PerfectLens and coverglass flats, built
+    with System.concatenate (17 history planes)."""
+    st = {"wavelength": 0.532, "aperture_radius_etl": 8, "aperture_radius": 50.8 / 2, "n_etl": 1.3,
+          "t_edge": 5, "f1": 160, "f2": 120, "fobj": 20, "t_coverglass": 1.25, "n_coverglass": 1.4585,
+          "dz_coverglass": 10, "n_immersion": 1.333}
+    t_center = st["t_edge"] + rad_curv * (1 - np.sqrt(1 - (st["aperture_radius_etl"] / rad_curv) ** 2))
+    rays = rt.get_collimated_rays([0, 0, -1], 8, nrays, st["wavelength"])
+    etl = rt.System([rt.FlatSurface([0, 0, 0], [0, 0, 1], st["aperture_radius_etl"]),
+                     rt.SphericalSurface.get_on_axis(-rad_curv, t_center, st["aperture_radius_etl"])],
+                    materials=[mat.Constant(st["n_etl"])], names="etl")
+    l1 = rt.System([rt.PerfectLens(st["f1"], [0, 0, 0], [0, 0, 1], alpha=np.arcsin(0.1))], [], names="l1")
+    l2 = rt.System([rt.PerfectLens(st["f2"], [0, 0, 0], [0, 0, 1], alpha=np.arcsin(0.1))], [], names="l2")
+    obj = rt.System([rt.PerfectLens(st["fobj"], [0, 0, 0], [0, 0, 1], alpha=np.arcsin(0.3))], [], names="obj")
+    cglass = rt.System([rt.FlatSurface([0, 0, 0], [0, 0, 1], st["aperture_radius"]),
+                        rt.FlatSurface([0, 0, st["t_coverglass"]], [0, 0, 1], st["aperture_radius"]),
+                        rt.FlatSurface([0, 0, 30], [0, 0, 1], st["aperture_radius"])],
+                       [mat.Constant(st["n_coverglass"]), mat.Constant(st["n_immersion"])], "coverglass")
+    osys = etl.concatenate(l1, mat.Vacuum(), st["f1"] - (t_center - st["t_edge"]))
+    osys = osys.concatenate(l2, mat.Vacuum(), st["f1"] + st["f2"])
+    osys = osys.concatenate(obj, mat.Vacuum(), st["f2"] + st["fobj"])
+    osys = osys.concatenate(cglass, mat.Vacuum(), st["dz_coverglass"])
+    return osys, rays, mat.Vacuum(), mat.Vacuum()
+
+
 # name -> recipe; every recipe returns (system, rays, initial_material, final_material)
 RECIPES = {
     "c1_plano_convex": c1_plano_convex,
@@ -366,4 +426,10 @@ RECIPES = {
     "stress": stress,
     "reversed_doublet": reversed_doublet,
     "tir_prism": tir_prism,
+    "astig_relay": astig_relay,
+    # the lightsheet script's first ETL radius (a hemisphere: sphere edge exactly at the aperture) and
+    # its last (1e9 mm, where the absolute 1e-12 on-sphere tolerance rejects rays, SURVEY §7 hard part 2)
+    "lightsheet_r8": lambda rt, mat: lightsheet(rt, mat, 8.0),
+    "lightsheet_r120": lambda rt, mat: lightsheet(rt, mat, 120.0),
+    "lightsheet_r1e9": lambda rt, mat: lightsheet(rt, mat, 1e9),
 }
