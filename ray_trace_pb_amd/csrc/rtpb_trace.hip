@@ -65,8 +65,15 @@ void trace_kernel(TraceArgs<TS> a) {
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
     uint4* tile_b = tiles[threadIdx.x >> 6][kFinal ? 0 : 1];
     Ray<T> r;
+#if defined(RTPB_EXP_NO_INPUT)             // experiment only: no input reads (write-only memory path)
+    {
+        const T v = T(i);
+        r.x = v; r.y = v; r.z = v; r.dx = v; r.dy = v; r.dz = v; r.ph = v; r.wl = T(0.5);
+    }
+#else
     if constexpr (kStaged && IN_LAYOUT == RTPB_AOS && (STORE & 4)) r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
     else r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
+#endif
     const T wl0 = r.wl;
     TS* __restrict__ out = a.out;
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
