@@ -50,6 +50,41 @@ __global__ __launch_bounds__(256) void planes_kernel(double* out, int64_t plane_
 // Persistent grid-stride form: `gridDim.x` one-wave workgroups; wave w handles units w, w + W, w + 2W, ...
 // (all planes of a unit before the next unit), so the concurrently running waves write the SAME plane at
 // neighbouring addresses, as a fill does.
+// 8-byte lanes (512 B per store instruction): `chunk` bytes per wave per stream in 512 B pieces.  With
+// streams = 88 and chunk = 512 this is the trace kernel's SoA output shape (8 fields x 11 planes).
+template <int kPieces>
+__global__ __launch_bounds__(256) void narrow_kernel(double* out, int64_t stream_stride_d, int streams, int64_t units) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    if (wave * kPieces >= units) return;
+    const double v = static_cast<double>(lane);
+    for (int p = 0; p < streams; ++p) {
+        double* base = out + p * stream_stride_d + wave * kPieces * 64;
+#pragma unroll
+        for (int c = 0; c < kPieces; ++c) __builtin_nontemporal_store(v + c, base + c * 64 + lane);
+    }
+}
+
+template <int kPieces>
+float run_narrow(double* buf, int64_t stream_bytes, int streams, int block, int reps) {
+    const int64_t units = stream_bytes / 512;
+    const int64_t waves = (units + kPieces - 1) / kPieces;
+    const dim3 grid(static_cast<unsigned>((waves * 64 + block - 1) / block));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    narrow_kernel<kPieces><<<grid, block>>>(buf, stream_bytes / 8, streams, units);
+    CHECK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) narrow_kernel<kPieces><<<grid, block>>>(buf, stream_bytes / 8, streams, units);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return ms / reps;
+}
+
 template <bool NT>
 __global__ __launch_bounds__(64) void persistent_kernel(double* out, int64_t plane_stride_d, int planes, int64_t units,
                                                         int spin) {
@@ -134,6 +169,12 @@ int main(int argc, char** argv) {
         {"persist P=11 W=5120", 11, -1, true, 0, 5120, 0},
         {"persist P=11 W=8192", 11, -1, true, 0, 8192, 0},
         {"persist P=11 W=5120 spin20", 11, -1, true, 0, 5120, 20},
+        // 8-byte lanes: chunks = -8 means 8 pieces of 512 B (4 KiB) per stream, -1... handled below
+        {"narrow P=11 4K wg64", 11, -8, true, 0, 64, 0},
+        {"narrow P=11 4K wg256", 11, -8, true, 0, 256, 0},
+        {"narrow P=88 512B wg64 (SoA)", 88, -9, true, 0, 64, 0},
+        {"narrow P=88 512B wg256 (SoA)", 88, -9, true, 0, 256, 0},
+        {"narrow P=1 4K wg64", 1, -8, true, 0, 64, 0},
     };
     for (int round = 0; round < 3; ++round) {
         for (const Case& c : cases) {
@@ -143,7 +184,9 @@ int main(int argc, char** argv) {
 #define DISPATCH(K)                                                                                   \
     ms = c.nt ? run<K, true>(buf, plane_bytes, stride, c.planes, c.block, c.spin, reps)               \
               : run<K, false>(buf, plane_bytes, stride, c.planes, c.block, c.spin, reps)
-            if (c.chunks < 0) ms = run_persistent(buf, plane_bytes, stride, c.planes, c.block, c.spin, reps);
+            if (c.chunks == -8) ms = run_narrow<8>(buf, plane_bytes, c.planes, c.block, reps);
+            else if (c.chunks == -9) ms = run_narrow<1>(buf, plane_bytes, c.planes, c.block, reps);
+            else if (c.chunks < 0) ms = run_persistent(buf, plane_bytes, stride, c.planes, c.block, c.spin, reps);
             else if (c.chunks == 4) DISPATCH(4);
             else if (c.chunks == 8) DISPATCH(8);
             else DISPATCH(16);
