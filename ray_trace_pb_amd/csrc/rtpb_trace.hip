@@ -58,8 +58,10 @@ void trace_kernel(TraceArgs<TS> a) {
     const int64_t ray0 = i - lane;                       // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
 #if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
-    if (blockIdx.x < RTPB_EXP_STAGGER)
-        for (unsigned k = 0; k < (blockIdx.x & 7u); ++k) __builtin_amdgcn_s_sleep(20);
+    // consecutive workgroups go to different XCDs, so the delay step uses blockIdx / 8 (varies inside
+    // an XCD); 0..7 steps of s_sleep(RTPB_EXP_STAGGER) (64 cycles per unit)
+    if (blockIdx.x < 8192)
+        for (unsigned k = 0; k < ((blockIdx.x >> 3) & 7u); ++k) __builtin_amdgcn_s_sleep(RTPB_EXP_STAGGER);
 #endif
     const bool valid = i < a.n;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
