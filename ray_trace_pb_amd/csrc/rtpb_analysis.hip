@@ -151,12 +151,13 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
     const cptr<double> table = (cptr<double>)(a.table);
     const double wl0 = rA.wl;                          // one wavelength per group
+    const Rcp<double> iwl = make_rcp(wl0);             // shared divisor of every phase update
     double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
     for (int s = 0; s < a.nsurf; ++s) {
         const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
         const DevSurface<double> sd = load_surface<double>(surf + s);
         Ray<double> aA, aB;
-        propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, aA, aB);
+        propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, iwl, iwl, aA, aB);
         rA = aA;
         rB = aB;
         n_cur = n_next;

@@ -108,6 +108,100 @@ RTPB_HD T np_sign(T v) {
     return v > T(0) ? T(1) : (v < T(0) ? T(-1) : (v == T(0) ? T(0) : v));
 }
 
+// ------------------------------------------------------------------ shared-divisor quotients
+// Several quotients a_i / b with ONE divisor (a vector normalised by its norm, a normal divided by the
+// radius, phases divided by the wavelength).  gfx950 has no f64 divide instruction; the compiler expands
+// every `a / b` into div_scale(b), rcp, four Newton FMAs (all on b only), div_scale(a), mul, fma,
+// div_fmas, div_fixup.  Rcp holds the b-only part (y = the same Newton-refined reciprocal, same
+// instructions) so each further quotient costs mul + fma + fma + div_fixup -- the compiler's own
+// sequence minus the scaling steps, which are identities when
+//   * b is 0, inf or NaN, or 2^-120 <= |b| <= 2^120, and
+//   * a is 0, inf or NaN, or 2^-800 <= |a| <= 2^600
+// (div_scale rescales only for |b| near the overflow/denormal range, a quotient in the denormal range,
+// an exponent gap >= 768 or |a| < 2^-969; div_fixup turns 0, inf and NaN operands into the IEEE result
+// on its own).  A lane outside those ranges takes the plain division, so every quotient is bit-identical
+// to `a / b`, i.e. correctly rounded.  Host builds (the CPU harness) always divide.
+template <typename T>
+struct Rcp {
+    T b;
+    T y;
+    bool ok;   // b in the range above (device); host: unused
+};
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTDIV)
+#define RTPB_FASTDIV 1
+__device__ __forceinline__ bool fastdiv_den_ok(double b) {
+    const double m = __builtin_fabs(b);
+    return (m >= 0x1p-120 && m <= 0x1p120) || __builtin_amdgcn_class(b, 0x267);   // 0x267: +-0, +-inf, NaN
+}
+__device__ __forceinline__ bool fastdiv_num_ok(double a) {
+    const double m = __builtin_fabs(a);
+    return (m >= 0x1p-800 && m <= 0x1p600) || __builtin_amdgcn_class(a, 0x267);
+}
+__device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
+    const double q0 = a * y;
+    const double e = __builtin_fma(-b, q0, a);
+    return __builtin_amdgcn_div_fixup(__builtin_fma(e, y, q0), b, a);
+}
+#endif
+
+template <typename T>
+RTPB_HD Rcp<T> make_rcp(T b) {
+#if defined(RTPB_FASTDIV)
+    if constexpr (sizeof(T) == 8) {
+        const double y0 = __builtin_amdgcn_rcp(b);
+        const double y1 = __builtin_fma(y0, __builtin_fma(-b, y0, 1.0), y0);
+        const double y2 = __builtin_fma(y1, __builtin_fma(-b, y1, 1.0), y1);
+        return Rcp<T>{b, y2, fastdiv_den_ok(b)};
+    }
+#endif
+    return Rcp<T>{b, T(0), true};
+}
+
+// a / r.b
+template <typename T>
+RTPB_HD T div1(T a, const Rcp<T>& r) {
+#if defined(RTPB_FASTDIV)
+    if constexpr (sizeof(T) == 8) {
+        T q = fastdiv_q(a, r.b, r.y);
+        if (__builtin_expect(!(r.ok && fastdiv_num_ok(a)), 0)) q = a / r.b;
+        return q;
+    }
+#endif
+    return a / r.b;
+}
+
+// a / b where r = make_rcp(b0) and b is b0 or NaN (a wavelength after its row was killed): a NaN b gives
+// NaN either way (div_fixup / the division), so y of b0 serves every value b can take
+template <typename T>
+RTPB_HD T div1_as(T a, T b, const Rcp<T>& r) {
+#if defined(RTPB_FASTDIV)
+    if constexpr (sizeof(T) == 8) {
+        T q = fastdiv_q(a, b, r.y);
+        if (__builtin_expect(!(r.ok && fastdiv_num_ok(a)), 0)) q = a / b;
+        return q;
+    }
+#endif
+    return a / b;
+}
+
+// (x, y, z) / r.b, one guard for the three quotients
+template <typename T>
+RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r) {
+#if defined(RTPB_FASTDIV)
+    if constexpr (sizeof(T) == 8) {
+        const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
+        if (__builtin_expect(!(r.ok && fastdiv_num_ok(x) && fastdiv_num_ok(y) && fastdiv_num_ok(z)), 0)) {
+            x = x / r.b; y = y / r.b; z = z / r.b;
+        } else {
+            x = qx; y = qy; z = qz;
+        }
+        return;
+    }
+#endif
+    x = x / r.b; y = y / r.b; z = z / r.b;
+}
+
 // ------------------------------------------------------------------ Material.n (MAT:39-144)
 // WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
 // budget); only valid for plans without POLY6 materials (rtpb_plan::lite).
@@ -159,7 +253,7 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
 template <typename T>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
-                        T* t_out = nullptr) {
+                        const Rcp<T>& iwl, T* t_out = nullptr) {
     const T t = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz) / (r.dx * nx + r.dy * ny + r.dz * nz);
     const T s = t < T(0) ? T(-1) : T(1);
     const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
@@ -169,7 +263,7 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     o.z = r.z + vz;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz);
-    o.ph = r.ph + dist * s * T(2) * T(Const<T>::pi) / r.wl * n;
+    o.ph = r.ph + div1_as(dist * s * T(2) * T(Const<T>::pi), r.wl, iwl) * n;
     o.wl = r.wl;
     if (exclude_backward && s == T(-1)) kill(o);
     if (t_out) *t_out = t;
@@ -178,7 +272,7 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
 
 // ------------------------------------------------------------------ SphericalSurface.get_intersect (RT:1479-1516)
 template <typename T>
-RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n) {
+RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl) {
     const T ox = r.x - s.c[0], oy = r.y - s.c[1], oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ox * ox + oy * oy + oz * oz - s.R2;
@@ -197,7 +291,7 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n) {
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
     const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz);
-    o.ph = r.ph + dist * T(2) * T(Const<T>::pi) / r.wl * n;
+    o.ph = r.ph + div1_as(dist * T(2) * T(Const<T>::pi), r.wl, iwl) * n;
     o.wl = r.wl;
     return o;
 }
@@ -210,7 +304,7 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
     const T inv = T(1) / nrm;
     x = x * inv; y = y * inv; z = z * inv;
 #else
-    x = x / nrm; y = y / nrm; z = z / nrm;
+    div3(x, y, z, make_rcp(nrm));
 #endif
     if (is_nan(x)) x = T(0);
     if (is_nan(y)) y = T(0);
@@ -302,22 +396,23 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
 template <typename T, int KIND, typename EmitAt>
-RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at, Ray<T>& after) {
+RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
+                          Ray<T>& after) {
     if constexpr (KIND == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
-        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false));   // "before" plane, RT:1790-1793
+        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl));   // "before" plane, RT:1790-1793
         const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
         const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
-        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false);
+        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
         const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz);
-        if (spn > T(1e-12)) { spx = spx / spn; spy = spy / spn; spz = spz / spn; }
+        if (spn > T(1e-12)) div3(spx, spy, spz, make_rcp(spn));
         const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
         const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z);
         T ux = r1x, uy = r1y, uz = r1z;
-        if (r1n != T(0)) { ux = ux / r1n; uy = uy / r1n; uz = uz / r1n; }
+        if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n));
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
         o.x = n1 * f * sin_t1 * spx + Bx;
@@ -331,20 +426,21 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, E
         o.wl = r.wl;
         if (tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a) kill(o);
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
-        const T k = T(Const<T>::two_pi) / r.wl;
+        const T k = div1_as(T(Const<T>::two_pi), r.wl, iwl);
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
-        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false);
+        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl);
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
         if constexpr (KIND == SPHERE) {
-            ri = sphere_hit(r, s, n1);
-            Nx = (ri.x - s.c[0]) / s.R;                                   // RT:1476
-            Ny = (ri.y - s.c[1]) / s.R;
-            Nz = (ri.z - s.c[2]) / s.R;
+            ri = sphere_hit(r, s, n1, iwl);
+            Nx = ri.x - s.c[0];                                            // (p - c) / R, RT:1476
+            Ny = ri.y - s.c[1];
+            Nz = ri.z - s.c[2];
+            div3(Nx, Ny, Nz, make_rcp(s.R));
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true);   // RT:1331-1337, 1398-1403
+            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl);   // RT:1331-1337, 1398-1403
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
@@ -365,40 +461,40 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, E
 // (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans without PerfectLens
 // surfaces (rtpb_plan::feat).
 template <typename T, bool WITH_LENS = true, typename EmitAt>
-RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, EmitAt&& emit_at,
-                                    Ray<T>& after) {
+RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
+                                    EmitAt&& emit_at, Ray<T>& after) {
     const int kind = s.kind;
-    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, emit_at, after);
-    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, emit_at, after);
-    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, emit_at, after);
-    else surface_step<T, FLAT>(s, r, n1, n2, emit_at, after);
+    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, iwl, emit_at, after);
+    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, iwl, emit_at, after);
+    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, iwl, emit_at, after);
+    else surface_step<T, FLAT>(s, r, n1, n2, iwl, emit_at, after);
 }
 
 // Two independent rays through the same surface: one kind dispatch, both bodies in one straight-line
 // region so the scheduler can interleave their dependency chains.
 template <typename T, bool WITH_LENS = true>
 RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, const Ray<T>& rb, T n1, T n2,
-                                    Ray<T>& after_a, Ray<T>& after_b) {
+                                    const Rcp<T>& iwl_a, const Rcp<T>& iwl_b, Ray<T>& after_a, Ray<T>& after_b) {
     auto none = [](const Ray<T>&) {};
     const int kind = s.kind;
     if (WITH_LENS && kind == PERFECT_LENS) {
-        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, none, after_a);
-        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, none, after_b);
+        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, iwl_a, none, after_a);
+        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, iwl_b, none, after_b);
     } else if (kind == SPHERE) {
-        surface_step<T, SPHERE>(s, ra, n1, n2, none, after_a);
-        surface_step<T, SPHERE>(s, rb, n1, n2, none, after_b);
+        surface_step<T, SPHERE>(s, ra, n1, n2, iwl_a, none, after_a);
+        surface_step<T, SPHERE>(s, rb, n1, n2, iwl_b, none, after_b);
     } else if (kind == PLANE_MIRROR) {
-        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, none, after_a);
-        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, none, after_b);
+        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, iwl_a, none, after_a);
+        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, iwl_b, none, after_b);
     } else {
-        surface_step<T, FLAT>(s, ra, n1, n2, none, after_a);
-        surface_step<T, FLAT>(s, rb, n1, n2, none, after_b);
+        surface_step<T, FLAT>(s, ra, n1, n2, iwl_a, none, after_a);
+        surface_step<T, FLAT>(s, rb, n1, n2, iwl_b, none, after_b);
     }
 }
 
 template <typename T, bool WITH_LENS = true>
 RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
-    propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, [&](const Ray<T>& v) { at = v; }, after);
+    propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, make_rcp(r.wl), [&](const Ray<T>& v) { at = v; }, after);
 }
 
 // ------------------------------------------------------------------ host: descriptor lowering

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(kTraceBlock) void plane_kernel(PlaneArgs a) {
         DevMaterial<double> m = *a.mat;
         const double n = material_n<double>(m, r.wl, a.table);
         double t;
-        const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0, &t);
+        const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0,
+                                                  make_rcp(r.wl), &t);
         tile_write<TS>(tile, lane, o);
         if (a.ts) a.ts[i] = t;
     }

@@ -77,6 +77,7 @@ void trace_kernel(TraceArgs<TS> a) {
     else r = load_ray<TS, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
 #endif
     const T wl0 = r.wl;
+    const Rcp<T> iwl = make_rcp(wl0);                    // shared divisor of every phase update
     TS* __restrict__ out = a.out;
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
     const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
@@ -86,7 +87,7 @@ void trace_kernel(TraceArgs<TS> a) {
         for (int s = 0; s < a.nsurf; ++s) {
             const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
             Ray<T> after;
-            propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next,
+            propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
                                                          [](const Ray<T>&) {}, after);
             r = after;
             n_cur = n_next;
@@ -135,7 +136,7 @@ void trace_kernel(TraceArgs<TS> a) {
         after.ph = r.ph + n_next + n_cur;
         emit_at(r);
 #else
-        propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, emit_at, after);
+        propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
 #endif
         if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip

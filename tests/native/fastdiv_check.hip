@@ -1,0 +1,61 @@
+// fastdiv_check.hip -- TEST INFRASTRUCTURE ONLY: runs the shared-divisor quotient helpers of
+// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3) on the GPU over caller-supplied
+// operand pairs, next to the compiler's own `a / b`, so tests/test_gpu_fastdiv.py can check that every
+// quotient is bit-identical to the IEEE division (NumPy's a / b) on adversarial inputs.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -I include \
+//         -o tests/native/_build/libfastdiv_check.so tests/native/fastdiv_check.hip
+#include <hip/hip_runtime.h>
+
+#include "../../ray_trace_pb_amd/csrc/rtpb_math.h"
+
+using namespace rtpb;
+
+namespace {
+
+// out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
+//      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i])
+__global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
+                             const unsigned char* kill, int64_t n, double* out) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double ai = a[i], bi = b[i];
+    const Rcp<double> r = make_rcp(bi);
+    out[i] = div1(ai, r);
+    out[n + i] = ai / bi;
+    double x = ai, y = a2[i], z = a3[i];
+    div3(x, y, z, r);
+    out[2 * n + i] = x;
+    out[3 * n + i] = y;
+    out[4 * n + i] = z;
+    const double bb = kill[i] ? __builtin_nan("") : bi;
+    out[5 * n + i] = div1_as(ai, bb, r);
+}
+
+}  // namespace
+
+extern "C" int fastdiv_check(const double* a, const double* a2, const double* a3, const double* b,
+                             const unsigned char* kill, int64_t n, double* out) {
+    const size_t bytes = static_cast<size_t>(n) * sizeof(double);
+    const double* src[4] = {a, a2, a3, b};
+    double* dev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double* dout = nullptr;
+    unsigned char* dk = nullptr;
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
+        e = hipMalloc(&dev[k], bytes);
+        if (e == hipSuccess) e = hipMemcpy(dev[k], src[k], bytes, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) e = hipMalloc(&dk, static_cast<size_t>(n));
+    if (e == hipSuccess) e = hipMemcpy(dk, kill, static_cast<size_t>(n), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&dout, 6 * bytes);
+    if (e == hipSuccess) {
+        check_kernel<<<static_cast<unsigned>((n + 255) / 256), 256>>>(dev[0], dev[1], dev[2], dev[3], dk, n, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, 6 * bytes, hipMemcpyDeviceToHost);
+    for (double* p : dev) (void)hipFree(p);
+    (void)hipFree(dk);
+    (void)hipFree(dout);
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}

@@ -44,3 +44,40 @@ def harness_trace(low, rays2d, dtype=np.float64):
                                      out.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
     return out
+
+
+FASTDIV_SRC = os.path.join(HERE, "native", "fastdiv_check.hip")
+FASTDIV_OUT = os.path.join(HERE, "native", "_build", "libfastdiv_check.so")
+_fastdiv = None
+
+
+def build_fastdiv():
+    """hipcc (gfx950) build of the GPU check of rtpb_math.h's shared-divisor quotients (run by
+    __graft_entry__.build(); the GPU box uses the prebuilt library)."""
+    deps = [FASTDIV_SRC] + DEPS[1:]
+    if os.path.exists(FASTDIV_OUT) and all(os.path.getmtime(FASTDIV_OUT) >= os.path.getmtime(d) for d in deps):
+        return FASTDIV_OUT
+    os.makedirs(os.path.dirname(FASTDIV_OUT), exist_ok=True)
+    tmp = f"{FASTDIV_OUT}.{os.getpid()}.tmp"
+    subprocess.run([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-ffp-contract=off", "-fPIC", "-shared", "-I", os.path.join(HERE, "..", "include"),
+                    "-o", tmp, FASTDIV_SRC], check=True)
+    os.replace(tmp, FASTDIV_OUT)
+    return FASTDIV_OUT
+
+
+def fastdiv_check(a, a2, a3, b, kill):
+    """(6, n) float64: div1, a / b, div3 x/y/z, div1_as -- computed on cuda:0."""
+    global _fastdiv
+    if _fastdiv is None:
+        import torch  # noqa: F401 -- one HIP runtime per process: bind to torch's
+        _fastdiv = ctypes.CDLL(build_fastdiv())
+        _fastdiv.fastdiv_check.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
+        _fastdiv.fastdiv_check.restype = ctypes.c_int
+    arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, a2, a3, b)]
+    k = np.ascontiguousarray(kill, dtype=np.uint8)
+    n = arrs[0].size
+    out = np.empty((6, n), dtype=np.float64)
+    rc = _fastdiv.fastdiv_check(*[x.ctypes.data for x in arrs], k.ctypes.data, n, out.ctypes.data)
+    assert rc == 0, rc
+    return out

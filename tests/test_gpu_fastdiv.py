@@ -1,0 +1,94 @@
+"""The kernels' shared-divisor quotients (rtpb_math.h make_rcp / div1 / div1_as / div3) are bit-identical
+to IEEE division (NumPy's a / b) on the GPU -- including the sign of zero -- on adversarial operands:
+random bit patterns over the whole double range, operands straddling the fast-path range limits,
+denormals, 0 / inf / NaN combinations, and realistic normalisation inputs (vector components over
+their norm).  The end-to-end bit-exact traces (test_gpu_parity.py) cover the same code in context."""
+import numpy as np
+import pytest
+
+import native_harness
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(got, exp):
+    """bitwise equal where exp is not NaN; NaN exactly where exp is NaN"""
+    nan = np.isnan(exp)
+    assert np.array_equal(np.isnan(got), nan)
+    g, e = got[~nan].view(np.uint64), exp[~nan].view(np.uint64)
+    bad = np.flatnonzero(g != e)
+    assert bad.size == 0, f"{bad.size} mismatches, first: got {got[~nan][bad[:4]]} expected {exp[~nan][bad[:4]]}"
+
+
+def _check(a, a2, a3, b, kill):
+    out = native_harness.fastdiv_check(a, a2, a3, b, kill)
+    with np.errstate(all="ignore"):
+        _same(out[1], a / b)             # the device's own division is IEEE
+        _same(out[0], a / b)             # div1
+        _same(out[2], a / b)             # div3
+        _same(out[3], a2 / b)
+        _same(out[4], a3 / b)
+        bb = np.where(kill.astype(bool), np.nan, b)
+        _same(out[5], a / bb)            # div1_as
+
+
+def _rand_bits(rng, n):
+    return rng.integers(0, 2**64, size=n, dtype=np.uint64, endpoint=False).view(np.float64)
+
+
+def _pow2_band(rng, n, lo, hi):
+    """signed values m * 2^k, m in [1, 2), k uniform in [lo, hi] (denormals where k < -1022)"""
+    k = rng.integers(lo, hi + 1, size=n)
+    m = 1.0 + rng.random(n)
+    s = np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    with np.errstate(over="ignore", under="ignore"):
+        return s * np.ldexp(m, k)
+
+
+def test_fastdiv_random_bit_patterns():
+    rng = np.random.default_rng(1)
+    n = 1 << 21
+    a, a2, a3, b = (_rand_bits(rng, n) for _ in range(4))
+    _check(a, a2, a3, b, rng.random(n) < 0.1)
+
+
+def test_fastdiv_range_edges():
+    rng = np.random.default_rng(2)
+    n = 1 << 21
+    bands_a = [(-1074, -1020), (-975, -960), (-806, -794), (-10, 10), (594, 606), (760, 780), (1010, 1023)]
+    bands_b = [(-1074, -1020), (-126, -114), (-10, 10), (114, 126), (1010, 1023)]
+    a = np.concatenate([_pow2_band(rng, n // len(bands_a) + 1, lo, hi) for lo, hi in bands_a])[:n]
+    b = np.concatenate([_pow2_band(rng, n // len(bands_b) + 1, lo, hi) for lo, hi in bands_b])[:n]
+    rng.shuffle(a)
+    rng.shuffle(b)
+    a2, a3 = rng.permutation(a), rng.permutation(a)
+    _check(a, a2, a3, b, rng.random(n) < 0.1)
+
+
+def test_fastdiv_specials():
+    vals = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 3.0, 5e-324, -5e-324, 2.2250738585072014e-308,
+                     1.7976931348623157e308, -1.7976931348623157e308, 2.0 ** (-800), 2.0 ** 600, 2.0 ** (-120), 2.0 ** 120,
+                     2.0 ** (-801), 2.0 ** 601, 2.0 ** (-121), 2.0 ** 121, 1e-12, 25.4, -100.0])
+    a, b = np.meshgrid(vals, vals)
+    a, b = a.ravel(), b.ravel()
+    a2, a3 = np.roll(a, 1), np.roll(a, 2)
+    kill = (np.arange(a.size) % 3 == 0)
+    _check(a, a2, a3, b, kill)
+
+
+def test_fastdiv_normalisation_inputs():
+    """what the kernels divide: vector components by their norm (tiny and zero components included),
+    positions by radii, phases by wavelengths"""
+    rng = np.random.default_rng(3)
+    n = 1 << 21
+    scale = 10.0 ** rng.uniform(-300, 300, size=(3, n))
+    v = rng.standard_normal((3, n)) * scale
+    v[0, ::7] = 0.0
+    v[1, ::5] = -0.0
+    v[2, ::11] = 1e-310
+    with np.errstate(all="ignore"):
+        nrm = np.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    _check(v[0], v[1], v[2], nrm, rng.random(n) < 0.05)
+    a = rng.uniform(-30, 30, n) * 10.0 ** rng.uniform(-16, 3, n)
+    b = rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(-4, 4, n)
+    _check(a, np.roll(a, 1), np.roll(a, 2), b, rng.random(n) < 0.05)

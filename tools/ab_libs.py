@@ -85,8 +85,24 @@ def main():
             C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
             lib.rtpb_timing_enable(0)
             times[(ln, name)].append(tot.value / cnt.value)
+    # every build must produce the same history as the base build (NaN where it has NaN, equal elsewhere)
+    mism = {}
+    for name, low, x, sel, out in cases:
+        ref = None
+        for ln in libs:
+            C._lib, E._PLANS = libs[ln], caches[ln]
+            E.trace_device(low, x, sel, out=out)
+            torch.cuda.synchronize()
+            got = out.clone()
+            if ref is None:
+                ref = got
+                continue
+            nan_r, nan_g = torch.isnan(ref), torch.isnan(got)
+            same = torch.equal(nan_r, nan_g) and torch.equal(ref[~nan_r], got[~nan_g])
+            mism[f"{ln}:{name}"] = "identical" if same else "DIFFERENT"
+            print(f"{ln:24s} {name:16s} output vs base: {mism[f'{ln}:{name}']}")
     C._lib, E._PLANS = libs["base"], caches["base"]
-    res = {}
+    res = {"outputs_vs_base": mism}
     for name, *_ in cases:
         base = float(np.median(times[("base", name)]))
         for ln in libs:
