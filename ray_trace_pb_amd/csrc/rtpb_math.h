@@ -73,8 +73,41 @@ template <> RTPB_HD float qnan<float>() { return __builtin_nanf(""); }
 
 template <typename T> RTPB_HD bool is_nan(T v) { return v != v; }
 
+// Device fast paths of the f64 division and square root that are bit-identical to the compiler's own
+// expansions (see "shared-divisor quotients" below and tsqrt); -DRTPB_NO_FASTDIV / -DRTPB_NO_FASTSQRT
+// build without them (A/B experiments).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTDIV)
+#define RTPB_FASTDIV 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTSQRT)
+#define RTPB_FASTSQRT 1
+#endif
+
 template <typename T> RTPB_HD T tsqrt(T v);
-template <> RTPB_HD double tsqrt<double>(double v) { return sqrt(v); }
+// gfx950 has no f64 sqrt instruction: the compiler emits (i) x < 2^-767 ? x * 2^256 : x, (ii) rsq + two
+// Goldschmidt/Newton rounds (mul, mul, 7 fma), (iii) the inverse rescale, and (iv) a select that returns
+// x itself for +-0 and +inf -- 18 instructions.  For 2^-767 <= x < inf, for x < 0 and for NaN, steps (i),
+// (iii) and (iv) are identities (a negative or NaN x gives NaN either way), so the device path runs step
+// (ii) alone -- the identical instructions, hence identical bits -- and hands the remaining inputs
+// (+-0, denormals, tiny normals, +inf) to the full expansion.
+template <> RTPB_HD double tsqrt<double>(double v) {
+#if defined(RTPB_FASTSQRT)
+    const double y = __builtin_amdgcn_rsq(v);
+    const double s0 = v * y;
+    const double h0 = y * 0.5;
+    const double r0 = __builtin_fma(-h0, s0, 0.5);
+    const double s1 = __builtin_fma(s0, r0, s0);
+    const double d0 = __builtin_fma(-s1, s1, v);
+    const double h1 = __builtin_fma(h0, r0, h0);
+    const double s2 = __builtin_fma(d0, h1, s1);
+    const double d1 = __builtin_fma(-s2, s2, v);
+    double s3 = __builtin_fma(d1, h1, s2);
+    if (__builtin_expect((v >= 0.0 && v < 0x1p-767) || v == __builtin_inf(), 0)) s3 = sqrt(v);
+    return s3;
+#else
+    return sqrt(v);
+#endif
+}
 template <> RTPB_HD float tsqrt<float>(float v) { return sqrtf(v); }
 
 template <typename T> RTPB_HD T tabs(T v) { return v < T(0) ? -v : (v == T(0) ? T(0) : v); }
@@ -128,8 +161,7 @@ struct Rcp {
     bool ok;   // b in the range above (device); host: unused
 };
 
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTDIV)
-#define RTPB_FASTDIV 1
+#if defined(RTPB_FASTDIV)
 __device__ __forceinline__ bool fastdiv_den_ok(double b) {
     const double m = __builtin_fabs(b);
     return (m >= 0x1p-120 && m <= 0x1p120) || __builtin_amdgcn_class(b, 0x267);   // 0x267: +-0, +-inf, NaN

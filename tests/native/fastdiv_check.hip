@@ -1,5 +1,5 @@
 // fastdiv_check.hip -- TEST INFRASTRUCTURE ONLY: runs the shared-divisor quotient helpers of
-// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3) on the GPU over caller-supplied
+// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3) and its square root (tsqrt) on the GPU over caller-supplied
 // operand pairs, next to the compiler's own `a / b`, so tests/test_gpu_fastdiv.py can check that every
 // quotient is bit-identical to the IEEE division (NumPy's a / b) on adversarial inputs.
 //
@@ -14,7 +14,7 @@ using namespace rtpb;
 namespace {
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
-//      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i])
+//      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a)
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -30,6 +30,8 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[4 * n + i] = z;
     const double bb = kill[i] ? __builtin_nan("") : bi;
     out[5 * n + i] = div1_as(ai, bb, r);
+    out[6 * n + i] = tsqrt<double>(bi);
+    out[7 * n + i] = tsqrt<double>(ai);
 }
 
 }  // namespace
@@ -48,12 +50,12 @@ extern "C" int fastdiv_check(const double* a, const double* a2, const double* a3
     }
     if (e == hipSuccess) e = hipMalloc(&dk, static_cast<size_t>(n));
     if (e == hipSuccess) e = hipMemcpy(dk, kill, static_cast<size_t>(n), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&dout, 6 * bytes);
+    if (e == hipSuccess) e = hipMalloc(&dout, 8 * bytes);
     if (e == hipSuccess) {
         check_kernel<<<static_cast<unsigned>((n + 255) / 256), 256>>>(dev[0], dev[1], dev[2], dev[3], dk, n, dout);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(out, dout, 6 * bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, 8 * bytes, hipMemcpyDeviceToHost);
     for (double* p : dev) (void)hipFree(p);
     (void)hipFree(dk);
     (void)hipFree(dout);

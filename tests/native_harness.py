@@ -67,7 +67,7 @@ def build_fastdiv():
 
 
 def fastdiv_check(a, a2, a3, b, kill):
-    """(6, n) float64: div1, a / b, div3 x/y/z, div1_as -- computed on cuda:0."""
+    """(8, n) float64: div1, a / b, div3 x/y/z, div1_as, tsqrt(b), tsqrt(a) -- computed on cuda:0."""
     global _fastdiv
     if _fastdiv is None:
         import torch  # noqa: F401 -- one HIP runtime per process: bind to torch's
@@ -77,7 +77,7 @@ def fastdiv_check(a, a2, a3, b, kill):
     arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, a2, a3, b)]
     k = np.ascontiguousarray(kill, dtype=np.uint8)
     n = arrs[0].size
-    out = np.empty((6, n), dtype=np.float64)
+    out = np.empty((8, n), dtype=np.float64)
     rc = _fastdiv.fastdiv_check(*[x.ctypes.data for x in arrs], k.ctypes.data, n, out.ctypes.data)
     assert rc == 0, rc
     return out

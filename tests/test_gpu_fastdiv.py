@@ -1,5 +1,5 @@
-"""The kernels' shared-divisor quotients (rtpb_math.h make_rcp / div1 / div1_as / div3) are bit-identical
-to IEEE division (NumPy's a / b) on the GPU -- including the sign of zero -- on adversarial operands:
+"""The kernels' shared-divisor quotients (rtpb_math.h make_rcp / div1 / div1_as / div3) and square root
+(tsqrt) are bit-identical to IEEE division and sqrt (NumPy's a / b, np.sqrt) on the GPU -- including the sign of zero -- on adversarial operands:
 random bit patterns over the whole double range, operands straddling the fast-path range limits,
 denormals, 0 / inf / NaN combinations, and realistic normalisation inputs (vector components over
 their norm).  The end-to-end bit-exact traces (test_gpu_parity.py) cover the same code in context."""
@@ -30,6 +30,8 @@ def _check(a, a2, a3, b, kill):
         _same(out[4], a3 / b)
         bb = np.where(kill.astype(bool), np.nan, b)
         _same(out[5], a / bb)            # div1_as
+        _same(out[6], np.sqrt(b))        # tsqrt
+        _same(out[7], np.sqrt(a))
 
 
 def _rand_bits(rng, n):
@@ -55,7 +57,7 @@ def test_fastdiv_random_bit_patterns():
 def test_fastdiv_range_edges():
     rng = np.random.default_rng(2)
     n = 1 << 21
-    bands_a = [(-1074, -1020), (-975, -960), (-806, -794), (-10, 10), (594, 606), (760, 780), (1010, 1023)]
+    bands_a = [(-1074, -1020), (-975, -960), (-806, -794), (-770, -764), (-10, 10), (594, 606), (760, 780), (1010, 1023)]
     bands_b = [(-1074, -1020), (-126, -114), (-10, 10), (114, 126), (1010, 1023)]
     a = np.concatenate([_pow2_band(rng, n // len(bands_a) + 1, lo, hi) for lo, hi in bands_a])[:n]
     b = np.concatenate([_pow2_band(rng, n // len(bands_b) + 1, lo, hi) for lo, hi in bands_b])[:n]
@@ -68,7 +70,8 @@ def test_fastdiv_range_edges():
 def test_fastdiv_specials():
     vals = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 3.0, 5e-324, -5e-324, 2.2250738585072014e-308,
                      1.7976931348623157e308, -1.7976931348623157e308, 2.0 ** (-800), 2.0 ** 600, 2.0 ** (-120), 2.0 ** 120,
-                     2.0 ** (-801), 2.0 ** 601, 2.0 ** (-121), 2.0 ** 121, 1e-12, 25.4, -100.0])
+                     2.0 ** (-801), 2.0 ** 601, 2.0 ** (-121), 2.0 ** 121, 1e-12, 25.4, -100.0, 2.0 ** (-767),
+                     np.nextafter(2.0 ** (-767), 0), np.nextafter(2.0 ** (-767), 1)])
     a, b = np.meshgrid(vals, vals)
     a, b = a.ravel(), b.ravel()
     a2, a3 = np.roll(a, 1), np.roll(a, 2)
