@@ -331,8 +331,9 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     const dim3 grid(static_cast<unsigned>((tiles + 1) / 2), static_cast<unsigned>(n_groups));
     auto go = [&](auto tag) {
         using TS = decltype(tag);
-        if (plan->feat == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
-        else if (plan->feat == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
+        const int f = plan->feat & 3;                 // lens / POLY6 code; tables are always compiled in here
+        if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
+        else if (f == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
         else hipLaunchKernelGGL((sweep_kernel<TS, 3>), grid, dim3(kBlock), 0, st, a);
     };
     if (plan->dtype == RTPB_F64) go(double{});

@@ -152,6 +152,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
         m.table = nullptr;
         p->mats.push_back(m);
     }
+    if (!p->table.empty()) p->feat |= (p->table.size() / 2 <= static_cast<size_t>(kLdsTablePairs)) ? 4 : 8;
     blob_layout<double>(*p);
     *plan_out = p;
     return RTPB_OK;

@@ -78,6 +78,7 @@ struct TraceArgs {
     uint64_t mask_lo;
     uint64_t mask_hi;
     int32_t nsurf;
+    int32_t ntable;       // (wavelength, n) pairs in `table`
 };
 
 // Descriptors are read-only for the whole launch: read them through the constant address space so
@@ -165,6 +166,13 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
 // Only the owning wave touches its tile and LDS executes one wave's DS operations in order, so no
 // workgroup barrier is needed -- just the lgkmcnt waits (asm, with a memory clobber so the compiler
 // cannot move the tile accesses across them).
+// Plans whose TABLE materials hold at most this many (wavelength, n) pairs in total get kernels that copy
+// the table into LDS at launch (rtpb_plan::feat bit 4), so the per-surface lookups are LDS reads.  A
+// global-memory lookup inside the surface loop costs far more than its latency: gfx950 counts loads and
+// stores in one in-order counter (vmcnt), so waiting for a table load also waits for every history
+// store the wave has in flight.
+constexpr int kLdsTablePairs = 256;
+
 constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -308,7 +316,9 @@ struct rtpb_plan {
     std::vector<rtpb_material> mats;    // table pointers cleared; see table_off/table_len
     std::vector<int32_t> table_off;
     std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
-    int feat = 0;                       // kernel features needed: 1 = PerfectLens, 2 = POLY6 material
+    // kernel features needed: 1 = PerfectLens, 2 = POLY6 material, 4 = TABLE materials whose table fits
+    // the kernel's LDS copy (kLdsTablePairs), 8 = TABLE materials read from global memory
+    int feat = 0;
     std::mutex mu;
     void* blob[rtpbi::kMaxDevices] = {};
     size_t off_mats = 0, off_table = 0, blob_bytes = 0;   // blob layout, fixed at plan creation

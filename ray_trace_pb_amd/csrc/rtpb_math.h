@@ -236,8 +236,9 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r) {
 
 // ------------------------------------------------------------------ Material.n (MAT:39-144)
 // WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
-// budget); only valid for plans without POLY6 materials (rtpb_plan::lite).
-template <typename T, bool WITH_POLY6 = true, typename TablePtr>
+// budget); WITH_TABLE = false compiles the TABLE case out.  Either is only valid for plans without such
+// materials (rtpb_plan::feat).
+template <typename T, bool WITH_POLY6 = true, bool WITH_TABLE = true, typename TablePtr>
 RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
     switch (m.kind) {
     case CONSTANT:
@@ -263,6 +264,7 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
         }
     }
     default: {                                                       // TABLE: host-evaluated n(lambda)
+        if constexpr (!WITH_TABLE) return qnan<T>();
         // (wavelength, n) pairs sorted by wavelength, NaN keys last (sort_table): binary search for
         // the exact wavelength; NaN compares false, so NaN keys behave as +inf in the search.
         const int len = m.table_len, off = m.table_off;

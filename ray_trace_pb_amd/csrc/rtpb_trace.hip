@@ -39,9 +39,12 @@ constexpr int trace_block(int out_layout, int store) {
 // The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic, TS
 // storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal global
 // stores for the staged tiles, bit 2 = LDS-staged AOS input loads, bit 3 = final plane only.
-// FEAT: bit 0 = PerfectLens code, bit 1 = RTPB_POLY6 code compiled in.  Leaving out what a plan does
-// not use lowers register pressure (f64 staged: 92 VGPRs without the PerfectLens code, 100 with both),
-// 10-15 % faster when compute-bound.  rtpb_plan::feat picks the variant.
+// FEAT: bit 0 = PerfectLens code, bit 1 = RTPB_POLY6 code compiled in, bit 2 = TABLE materials looked up
+// in an LDS copy of the plan's table (dynamic LDS, copied at launch), bit 3 = TABLE materials looked up
+// in global memory.  Leaving out what a plan does not use lowers register pressure (f64 staged: 92 VGPRs
+// without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
+// table lookup the surface loop never waits on the vmcnt counter, which on gfx950 would also wait for
+// every history store in flight (see kLdsTablePairs).  rtpb_plan::feat picks the variant.
 template <typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
 __global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 void trace_kernel(TraceArgs<TS> a) {
@@ -52,7 +55,17 @@ void trace_kernel(TraceArgs<TS> a) {
     // STORE bit 3: only the final plane is stored (planes='final'): no per-surface store logic, one
     // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
     constexpr bool kFinal = (STORE & 8) != 0;
-    __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16];  // per wave: "at" and "after" tiles
+    constexpr bool kLens = (FEAT & 1) != 0, kPoly = (FEAT & 2) != 0;
+    constexpr bool kTabLds = (FEAT & 12) == 4, kTabGlobal = (FEAT & 8) != 0;
+    extern __shared__ double lds_table[];                // FEAT bit 2: the plan's (wavelength, n) pairs
+    if constexpr (kTabLds) {
+        // before any wave can leave: the unstaged variants run four-wave workgroups and need the barrier
+        for (int k = threadIdx.x; k < 2 * a.ntable; k += kB) lds_table[k] = a.table[k];
+        if constexpr (kB > 64) __syncthreads();
+    }
+    // per wave: "at" and "after" tiles of 64 records (4 KiB f64, 2 KiB f32: the LDS budget allows 5 f64 /
+    // 10 f32 waves per SIMD in the all-planes mode, so registers set the f32 occupancy)
+    __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16 * sizeof(TS) / 8];
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
     const int64_t ray0 = i - lane;                       // first ray of this wave
@@ -82,12 +95,16 @@ void trace_kernel(TraceArgs<TS> a) {
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
     const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
     const cptr<T> table = (cptr<T>)(a.table);
+    auto mat_n = [&](cptr<DevMaterial<T>> mp) -> T {
+        if constexpr (kTabLds) return material_n<T, kPoly, true>(load_material<T>(mp), wl0, lds_table);
+        else return material_n<T, kPoly, kTabGlobal>(load_material<T>(mp), wl0, table);
+    };
     if constexpr (kFinal) {
-        T n_cur = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats), wl0, table);
+        T n_cur = mat_n(mats);
         for (int s = 0; s < a.nsurf; ++s) {
-            const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
+            const T n_next = mat_n(mats + s + 1);
             Ray<T> after;
-            propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
+            propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
                                                          [](const Ray<T>&) {}, after);
             r = after;
             n_cur = n_next;
@@ -112,9 +129,9 @@ void trace_kernel(TraceArgs<TS> a) {
         }
         slot_off += a.out_ps;
     }
-    T n_cur = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats), wl0, table);
+    T n_cur = mat_n(mats);
     for (int s = 0; s < a.nsurf; ++s) {
-        const T n_next = material_n<T, (FEAT & 2) != 0>(load_material<T>(mats + s + 1), wl0, table);
+        const T n_next = mat_n(mats + s + 1);
         const int p = 2 * s + 1;
         const bool st_at = plane_bit(a.mask_lo, a.mask_hi, p);          // wave-uniform
         const bool st_after = plane_bit(a.mask_lo, a.mask_hi, p + 1);
@@ -136,7 +153,7 @@ void trace_kernel(TraceArgs<TS> a) {
         after.ph = r.ph + n_next + n_cur;
         emit_at(r);
 #else
-        propagate_surface_emit<T, (FEAT & 1) != 0>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
+        propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
 #endif
         if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
@@ -174,8 +191,9 @@ template <typename T, int IL, int OL, int ST, int W, int FEAT>
 hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
     constexpr int kB = trace_block(OL, ST);
     const int64_t blocks = (a.n + kB - 1) / kB;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), 0, st,
-                       a);
+    const size_t lds = (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), lds,
+                       st, a);
     return hipGetLastError();
 }
 
@@ -183,11 +201,20 @@ template <typename T, int IL, int OL, int ST>
 hipError_t launch_one(const TraceArgs<T>& a, int feat, hipStream_t st) {
     if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
         const int w = g_waves_per_eu.load();
-        if (w == 5) return launch_w<T, IL, OL, ST, 5, 3>(a, st);
+        if (w == 5) return launch_w<T, IL, OL, ST, 5, 15>(a, st);
     }
-    if (feat == 0) return launch_w<T, IL, OL, ST, 1, 0>(a, st);
-    if (feat == 1) return launch_w<T, IL, OL, ST, 1, 1>(a, st);
-    return launch_w<T, IL, OL, ST, 1, 3>(a, st);
+#if defined(RTPB_EXP_WPE)                  // experiment only: minimum waves per SIMD for every variant
+    constexpr int kW = RTPB_EXP_WPE;
+#else
+    constexpr int kW = 1;
+#endif
+    switch (feat) {
+    case 0: return launch_w<T, IL, OL, ST, kW, 0>(a, st);
+    case 1: return launch_w<T, IL, OL, ST, kW, 1>(a, st);
+    case 4: return launch_w<T, IL, OL, ST, kW, 4>(a, st);
+    case 5: return launch_w<T, IL, OL, ST, kW, 5>(a, st);
+    default: return launch_w<T, IL, OL, ST, kW, 15>(a, st);    // POLY6 or a large table: everything in
+    }
 }
 
 template <typename T>
@@ -233,6 +260,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int64_t n, int il, int6
         a.mask_lo = lo;
         a.mask_hi = hi;
         a.nsurf = plan->nsurf;
+        a.ntable = static_cast<int32_t>(plan->table.size() / 2);
         return launch_trace<TS>(a, il, ol, plan->feat, st);
     };
     hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -51,6 +51,8 @@ def main():
     recipes = {"c2": lambda: (systems.c2_system(rt, mat), systems.c2_rays(args.rays), mat.Vacuum(), mat.Vacuum()),
                "c5": lambda: (systems.c5_system(rt, mat),
                               systems.c5_rays(rt, 1, 101, max(1, args.rays // 707)), mat.Constant(1), mat.Constant(1)),
+               "c3": lambda: (systems.c3_system(rt, mat), systems.c3_rays(rt, 1001, max(1, args.rays // 5005)),
+                              mat.Vacuum(), mat.Vacuum()),
                "c4": lambda: (systems.c4_system(rt, mat), systems.c4_rays(rt, 1001, max(1, args.rays // 1001)),
                               mat.Constant(systems.OPM_N1), mat.Vacuum())}
     cases = []
