@@ -67,7 +67,16 @@ void trace_kernel(TraceArgs<TS> a) {
     // 10 f32 waves per SIMD in the all-planes mode, so registers set the f32 occupancy)
     __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16 * sizeof(TS) / 8];
     const int lane = threadIdx.x & 63;
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
+    // one block of kB rays (the whole kernel, or one step of the persistent experiment's loop)
+    auto body = [&](const int64_t blk) {
+#if defined(RTPB_EXP_XCD_REMAP)             // experiment only: each XCD takes a contiguous range of ray blocks
+    // workgroups are dispatched round-robin over the 8 XCDs: block b runs on XCD b % 8
+    const uint32_t nb = gridDim.x, per = nb / 8, xcd = blockIdx.x % 8, k = blockIdx.x / 8;
+    const uint32_t bid = blockIdx.x < per * 8 ? xcd * per + k : blockIdx.x;
+    const int64_t i = static_cast<int64_t>(bid) * kB + threadIdx.x;
+#else
+    const int64_t i = blk * kB + threadIdx.x;
+#endif
     const int64_t ray0 = i - lane;                       // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
 #if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
@@ -167,6 +176,12 @@ void trace_kernel(TraceArgs<TS> a) {
         r = after;
         n_cur = n_next;
     }
+    };
+#if defined(RTPB_EXP_PERSIST)              // experiment only: persistent grid, block-stride loop
+    for (int64_t blk = blockIdx.x; blk * kB < a.n; blk += gridDim.x) body(blk);
+#else
+    body(static_cast<int64_t>(blockIdx.x));
+#endif
 }
 
 
@@ -192,7 +207,20 @@ hipError_t launch_w(const TraceArgs<T>& a, hipStream_t st) {
     constexpr int kB = trace_block(OL, ST);
     const int64_t blocks = (a.n + kB - 1) / kB;
     const size_t lds = (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
-    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), lds,
+#if defined(RTPB_EXP_PERSIST)
+    static int resident = 0;                     // experiment: one wave slot per workgroup of the grid
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<T, IL, OL, ST, W, FEAT>, kB, lds);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident = per_cu * cus * RTPB_EXP_PERSIST;
+    }
+    const int64_t grid = blocks < resident ? blocks : resident;
+#else
+    const int64_t grid = blocks;
+#endif
+    hipLaunchKernelGGL((trace_kernel<T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(grid)), dim3(kB), lds,
                        st, a);
     return hipGetLastError();
 }
