@@ -429,6 +429,42 @@ def test_material_dispersion_bitwise_over_wavelength_sweep(material):
     assert np.array_equal(got, ref, equal_nan=True)
 
 
+@pytest.mark.parametrize("n_wl", [1, 127, 128, 129, 255, 256, 257])
+def test_table_materials_lds_and_global_lookup(n_wl):
+    """TABLE materials (Ebaf11 + a user Material subclass) around the LDS-table size limit: kernels copy
+    the plan's (wavelength, n) pairs into LDS when all of them fit (kLdsTablePairs = 256 pairs in total,
+    here 2 * n_wl), else they search global memory.  Every variant is bit-exact vs the oracle: NumPy path,
+    torch path, float32 storage, and the unstaged four-wave-workgroup kernels."""
+    system = rt.System([rt.FlatSurface([0, 0, 0], [0, 0, 1], 50),
+                        rt.SphericalSurface.get_on_axis(40.0, 5.0, 30.0),
+                        rt.FlatSurface([0, 0, 12], systems.unit([0.1, 0, 1]), 50)],
+                       [mat.Ebaf11(), systems.cauchy_class(mat)()])
+    rng = np.random.default_rng(n_wl)
+    n = 4099
+    rays = np.zeros((n, 8))
+    rays[:, 0:2] = rng.uniform(-8, 8, (n, 2))
+    rays[:, 2] = -1.0
+    d = np.stack((rng.normal(scale=0.05, size=n), rng.normal(scale=0.05, size=n), np.ones(n)), axis=1)
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1)[:, None]
+    wls = np.linspace(0.4, 1.6, n_wl)
+    rays[:, 7] = wls[rng.integers(0, n_wl, n)]
+    m0, m1 = mat.Vacuum(), mat.Vacuum()
+    ref = oracle(system, m0, m1, rays)
+    assert np.array_equal(system.ray_trace(rays, m0, m1), ref, equal_nan=True)
+    x = torch.from_numpy(rays).to(DEV)
+    assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), ref, equal_nan=True)
+    r32 = rays.astype(np.float32)
+    exp32 = oracle(system, m0, m1, r32.astype(np.float64)).astype(np.float32)
+    got32 = system.ray_trace(torch.from_numpy(r32).to(DEV), m0, m1, dtype="float32").cpu().numpy()
+    assert np.array_equal(got32, exp32, equal_nan=True)
+    lib = C.lib()
+    C.check(lib.rtpb_set_tuning(b"aos_staging", 0))
+    try:
+        assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), ref, equal_nan=True)
+    finally:
+        C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
+
+
 def test_more_than_2_31_rays_in_one_launch():
     """Maximum sizes: one trace of 2^31 + 4633 rays (int64 ray indexing, > 2^25 workgroups), float32
     storage, final plane only (68.7 GB in + 68.7 GB out of HBM).  Rays on both sides of index 2^31 and
