@@ -243,6 +243,19 @@ def main():
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
 
+    # the same output buffer written by a plain fill (one contiguous stream): the delivered write rate of
+    # this placement, for context (the multi-plane history is placement-sensitive, fill is not)
+    if rank == 0:
+        out.fill_(0.0)
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record()
+        for _ in range(10):
+            out.fill_(0.0)
+        f1.record()
+        torch.cuda.synchronize()
+        fill_ms = f0.elapsed_time(f1) / 10
+        fill_gbs = out.numel() * out.element_size() / (fill_ms * 1e-3) / 1e9
+
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -286,7 +299,8 @@ def main():
                          "traffic": (traffic / 1.0) if traffic is not None else None,
                          "kernel": "trace_kernel", "kernel_ms_avg": kernel_ms, "kernel_ms_max_rank": kernel_ms_max,
                          "kernel_ms_method": "HIP events on the launch stream around the K launches / K",
-                         "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_ray_surface": bytes_per_ray / S},
+                         "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_ray_surface": bytes_per_ray / S,
+                         "output_fill_GBps": fill_gbs, "frac_of_output_fill": achieved / fill_gbs},
             "cpu_baseline": cpu,
         }
         if traffic_note:

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--rays", type=int, default=1_000_000)
     ap.add_argument("--libs", default="", help="comma list of experiment builds timed on the same buffers")
     ap.add_argument("--kinds", default="torch,hipExtMalloc,contiguous")
+    ap.add_argument("--tunings", default="", help="comma list of knob=value variants of the base library "
+                                                   "(rtpb_set_tuning), e.g. nt_stores=0")
     ap.add_argument("--order", default="random", choices=["random", "seq"],
                     help="seq: buffers in allocation order (PMC runs map dispatches to buffers by index)")
     args = ap.parse_args()
@@ -86,12 +88,21 @@ def main():
             with E.plan_ref(low) as plan:
                 C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), x.shape[0], C.RTPB_AOS, 0, ptr, C.RTPB_AOS,
                                        8 * x.shape[0], x.shape[0], lo, hi, torch.cuda.current_stream().cuda_stream))
+        tun = {ln: (None, None) for ln in libs}
+        for t in filter(None, args.tunings.split(",")):
+            knob, val = t.split("=")
+            libs[f"base+{t}"] = libs["base"]
+            tun[f"base+{t}"] = (knob.encode(), int(val))
+        defaults = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0}
         items = [(ln, b) for ln in libs for b in range(len(outs))]
         times = {it: [] for it in items}
         for _ in range(args.rounds):
             for ii in (rng.permutation(len(items)) if args.order == "random" else range(len(items))):
                 ln, b = items[ii]
                 lib = libs[ln]
+                knob, val = tun[ln]
+                if knob:
+                    C.check(lib.rtpb_set_tuning(knob, val))
                 run(lib, outs[b][0])
                 torch.cuda.synchronize()
                 lib.rtpb_timing_enable(1)
@@ -100,6 +111,8 @@ def main():
                 tot, cnt = ctypes.c_double(), ctypes.c_int64()
                 C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
                 lib.rtpb_timing_enable(0)
+                if knob:
+                    C.check(lib.rtpb_set_tuning(knob, defaults[knob.decode()]))
                 times[(ln, b)].append(tot.value / cnt.value)
         C._lib, E._PLANS = libs["base"], caches["base"]
         # the same buffers written by a plain fill (one contiguous stream): is the spread the kernel's?
