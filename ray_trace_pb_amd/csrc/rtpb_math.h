@@ -285,10 +285,13 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
 
 // ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
+// iden: optional make_rcp of the denominator d.nrm, shared by several planes with the same normal.
 template <typename T>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
-                        const Rcp<T>& iwl, T* t_out = nullptr) {
-    const T t = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz) / (r.dx * nx + r.dy * ny + r.dz * nz);
+                        const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr) {
+    const T num = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz);
+    const T den = r.dx * nx + r.dy * ny + r.dz * nz;
+    const T t = iden ? div1_as(num, den, *iden) : num / den;
     const T s = t < T(0) ? T(-1) : T(1);
     const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
     Ray<T> o;
@@ -435,10 +438,12 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
     if constexpr (KIND == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
-        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl));   // "before" plane, RT:1790-1793
+        // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
+        const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
+        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden));   // RT:1790-1793
         const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
         const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
-        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl);
+        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
         const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz);

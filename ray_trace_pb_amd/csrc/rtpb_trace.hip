@@ -74,6 +74,11 @@ void trace_kernel(TraceArgs<TS> a) {
     const uint32_t nb = gridDim.x, per = nb / 8, xcd = blockIdx.x % 8, k = blockIdx.x / 8;
     const uint32_t bid = blockIdx.x < per * 8 ? xcd * per + k : blockIdx.x;
     const int64_t i = static_cast<int64_t>(bid) * kB + threadIdx.x;
+#elif defined(RTPB_EXP_SCATTER)           // experiment only: ray blocks visited in a scattered order
+    // block b -> (b * RTPB_EXP_SCATTER) mod nb, a bijection when nb is not a multiple of the prime
+    const int64_t nb = gridDim.x;
+    const int64_t bs = (nb % RTPB_EXP_SCATTER) ? (blk * RTPB_EXP_SCATTER) % nb : blk;
+    const int64_t i = bs * kB + threadIdx.x;
 #else
     const int64_t i = blk * kB + threadIdx.x;
 #endif
