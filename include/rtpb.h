@@ -39,7 +39,8 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 2   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup */
+#define RTPB_ABI_VERSION 3   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+                                3: input element type separate from the storage type (in_dtype) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -115,9 +116,11 @@ int rtpb_shutdown(void);
 
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
 /* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,
-   System.materials, final material).  `dtype` is the STORAGE type of the ray buffers, RTPB_F64 or
-   RTPB_F32; arithmetic is always float64 (the reference's numerics), so an RTPB_F32 trace returns the
-   float64 result for the float32-rounded input, rounded once to float32 on store. */
+   System.materials, final material).  `dtype` is the STORAGE type of the output history, RTPB_F64 or
+   RTPB_F32; arithmetic is always float64 (the reference's numerics).  The input rays keep their own
+   element type (`in_dtype` of the trace calls): float64 rays traced into an RTPB_F32 plan give the
+   reference's float64 history rounded once to float32 (nothing is rounded before the arithmetic), and
+   float32 rays are widened exactly, as NumPy promotes them in the reference. */
 int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf,
                      const rtpb_material* materials, int32_t nmat,
                      int32_t dtype, rtpb_plan** plan_out);
@@ -126,23 +129,25 @@ int rtpb_plan_destroy(rtpb_plan* plan);
 /* ---- tracing on device-resident buffers ----------------------------------------------------- */
 /* Trace n_rays rays through the whole plan on `device`, asynchronously on `stream` (a hipStream_t,
    NULL = the device's null stream).
-     rays_in          device pointer, n_rays rays in `in_layout`; SOA fields are `in_field_stride`
-                      elements apart (>= n_rays).
+     rays_in          device pointer, n_rays rays in `in_layout` with elements of type `in_dtype`
+                      (RTPB_F64 / RTPB_F32; SOA input must use the plan's dtype); SOA fields are
+                      `in_field_stride` elements apart (>= n_rays).
      out              device pointer to slot 0 of the output; slots are `out_plane_stride` elements
                       apart (>= 8*n_rays); SOA fields are `out_field_stride` elements apart.
      plane_mask_lo/hi bits 0..63 / 64..127 select history planes 0..2S (see above).
-   The element type of every buffer is the plan's dtype. */
+   The output's element type is the plan's dtype. */
 int rtpb_trace(const rtpb_plan* plan, int32_t device,
-               const void* rays_in, int64_t n_rays, int32_t in_layout, int64_t in_field_stride,
+               const void* rays_in, int32_t in_dtype, int64_t n_rays, int32_t in_layout, int64_t in_field_stride,
                void* out, int32_t out_layout, int64_t out_plane_stride, int64_t out_field_stride,
                uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream);
 
 /* ---- tracing host buffers (NumPy in, NumPy out), sharded over several GPUs ------------------ */
-/* rays_in: host, n_rays x 8 AOS.  out: host, nslots x n_rays x 8 AOS (nslots = popcount of the mask).
+/* rays_in: host, n_rays x 8 AOS of `in_dtype`.  out: host, nslots x n_rays x 8 AOS of the plan's dtype
+   (nslots = popcount of the mask).
    Rays are split into contiguous index ranges, one per listed device (NULL/0 devices = device 0),
    each traced by its own host thread with chunked, double-buffered H2D / kernel / D2H copies.
    Synchronous: returns when `out` is complete. */
-int rtpb_trace_host(const rtpb_plan* plan, const void* rays_in, int64_t n_rays, void* out,
+int rtpb_trace_host(const rtpb_plan* plan, const void* rays_in, int32_t in_dtype, int64_t n_rays, void* out,
                     uint64_t plane_mask_lo, uint64_t plane_mask_hi,
                     const int32_t* devices, int32_t n_devices);
 

@@ -229,12 +229,22 @@ def host_empty(shape, dtype):
     return np.empty(shape, dtype=dtype)
 
 
+def input_code(dt):
+    """Element type the kernel reads the input rays in: float32 rays as they are (widened exactly in
+    the kernel, as NumPy promotes them in the reference), everything else as float64.  Independent of
+    the storage type, so float64 rays are never rounded before the arithmetic."""
+    name = str(dt).replace("torch.", "")
+    return C.RTPB_F32 if name == "float32" else C.RTPB_F64
+
+
 def trace_host(low, rays2d, planes, devices=None, out=None):
-    """NumPy (N, 8) -> NumPy (len(planes), N, 8)."""
-    rays2d = np.ascontiguousarray(rays2d, dtype=_np_dtype(low.dtype))
+    """NumPy (N, 8) -> NumPy (len(planes), N, 8) of the plan's storage type."""
+    rays2d = np.asarray(rays2d)
+    in_code = input_code(rays2d.dtype)
+    rays2d = np.ascontiguousarray(rays2d, dtype=_np_dtype(in_code))
     n = rays2d.shape[0]
     if out is None:
-        out = host_empty((len(planes), n, 8), rays2d.dtype)
+        out = host_empty((len(planes), n, 8), _np_dtype(low.dtype))
     lo, hi = plane_mask(planes)
     if devices is None:
         devs = None
@@ -243,15 +253,17 @@ def trace_host(low, rays2d, planes, devices=None, out=None):
         devs = (ctypes.c_int32 * len(devices))(*devices)
         ndev = len(devices)
     with plan_ref(low) as plan:
-        C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, n, out.ctypes.data, lo, hi, devs, ndev))
+        C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, in_code, n, out.ctypes.data, lo, hi, devs, ndev))
     return out
 
 
 def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None):
-    """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA]."""
+    """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA] of the
+    plan's storage type."""
     import torch
     tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
-    rays = rays.to(dtype=tdt).contiguous()
+    in_code = input_code(rays.dtype)
+    rays = rays.to(dtype=torch.float32 if in_code == C.RTPB_F32 else torch.float64).contiguous()
     n = rays.shape[0]
     if out is None:
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
@@ -260,6 +272,6 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     if stream is None:
         stream = torch.cuda.current_stream(rays.device).cuda_stream
     with plan_ref(low) as plan:
-        C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), n, C.RTPB_AOS, 0,
+        C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
                                    out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
     return out

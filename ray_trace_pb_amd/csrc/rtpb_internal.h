@@ -64,9 +64,12 @@ struct DeviceGuard {
 };
 
 // ---------------------------------------------------------------------------------- kernel args
-template <typename TS>
+// TIN: element type of the input rays, TS: storage type of the output planes (the plan's dtype).  They
+// differ when float64 rays are stored as float32 history (or float32 rays as float64): the input is read
+// as given, so no value is rounded before the float64 arithmetic.
+template <typename TIN, typename TS>
 struct TraceArgs {
-    const TS* __restrict__ in;
+    const TIN* __restrict__ in;
     TS* __restrict__ out;
     const DevSurface<double>* __restrict__ surf;
     const DevMaterial<double>* __restrict__ mats;
@@ -80,6 +83,18 @@ struct TraceArgs {
     int32_t nsurf;
     int32_t ntable;       // (wavelength, n) pairs in `table`
 };
+
+// The trace kernel's launcher for one (input, storage) type pair: picks the kernel variant for the
+// layouts, the tuning knobs and the plan's features (rtpb_trace_kernel.h; instantiated in
+// rtpb_trace_<tin>_<ts>.hip).
+template <typename TIN, typename TS>
+hipError_t launch_trace(const TraceArgs<TIN, TS>& a, int il, int ol, int feat, hipStream_t st);
+extern template hipError_t launch_trace<double, double>(const TraceArgs<double, double>&, int, int, int, hipStream_t);
+extern template hipError_t launch_trace<float, float>(const TraceArgs<float, float>&, int, int, int, hipStream_t);
+extern template hipError_t launch_trace<double, float>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
+extern template hipError_t launch_trace<float, double>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
+// tuning knobs (rtpb_set_tuning, defined in rtpb_trace.hip)
+extern std::atomic<int> g_aos_staging, g_nt_stores, g_waves_per_eu, g_stage_input, g_host_chunk_mib;
 
 // Descriptors are read-only for the whole launch: read them through the constant address space so
 // the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.

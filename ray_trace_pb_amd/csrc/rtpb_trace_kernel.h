@@ -1,0 +1,273 @@
+// rtpb_trace_kernel.h -- the fused trace kernel (the hot path) and its launch dispatch, templated on
+// the input element type TIN and the storage type TS.  Each rtpb_trace_<tin>_<ts>.hip translation unit
+// instantiates launch_trace for one (TIN, TS) pair so the variants compile in parallel; the host side
+// (rtpb_trace.hip) only sees the declaration in rtpb_internal.h.
+//
+// plan (replacing System.ray_trace's surface loop RT:658-659 and the per-surface NumPy ufunc chains of
+// RT:1160-1801), plus the host-buffer pipeline, tuning knobs and launch timing of the C ABI.
+// Hot path: ONE kernel launch traces every ray through every surface of the system (replacing the
+// Python surface loop RT:658-659 and the per-surface NumPy ufunc chains of RT:1160-1801).  One lane
+// owns one ray for the whole system:
+//   * the ray record (8 values) is read once from HBM (AOS: 16-byte vector loads; SOA: coalesced
+//     per-field loads) and kept in VGPRs;
+//   * surface and material descriptors are wave-uniform -- they are read through constant-address-
+//     space pointers with uniform indices, i.e. scalar loads (s_load) into SGPRs, once per wave;
+//   * n(lambda) of every material is evaluated once per ray (the reference re-evaluates it 3-4x per
+//     surface, MAT:39-51 via RT:297/1213/1512) and carried across the surface loop;
+//   * every requested history plane is written exactly once, at its final location -- no
+//     O(S^2 N) re-copying of the history (RT:1229-1232);
+//   * per-ray failures are NaN selects, never divergent early exits, so a wave stays converged.
+// The surface loop is wave-uniform (same system for every lane), so its `kind` switches never diverge.
+//
+// Precision: arithmetic is ALWAYS float64 in registers (the reference's numerics); the storage type TS
+// of the ray buffers is float64 or float32.  float32 storage halves the HBM bytes (the bound) while the
+// values stay the correctly rounded float64 results: a float32 trace equals the float64 reference on the
+// float32-rounded input, rounded once on store.
+//
+// Memory roofline: per ray the kernel moves 8w bytes in and 8w bytes per stored plane out
+// (w = sizeof(TS)); see DESIGN.md for the algorithmic-byte accounting used by bench.py.
+
+#pragma once
+
+#include "rtpb_internal.h"
+
+namespace rtpbi {
+
+
+// Workgroup size per variant: the LDS-staged AoS kernels run one wave per workgroup (see kTraceBlock);
+// the direct-store variants (SoA output, unstaged AoS) keep four-wave workgroups, which measured faster
+// for their strided stores (C5 SoA: 0.53 vs 0.69 ms).
+constexpr int trace_block(int out_layout, int store) {
+    return (out_layout == RTPB_AOS && (store & 1)) ? kTraceBlock : 256;
+}
+
+// The fused multi-surface trace: one lane = one ray through all surfaces (float64 arithmetic, TS
+// storage).  STORE: bit 0 = LDS-staged AOS stores (OUT_LAYOUT == AOS only), bit 1 = non-temporal global
+// stores for the staged tiles, bit 2 = LDS-staged AOS input loads, bit 3 = final plane only.
+// FEAT: bit 0 = PerfectLens code, bit 1 = RTPB_POLY6 code compiled in, bit 2 = TABLE materials looked up
+// in an LDS copy of the plan's table (dynamic LDS, copied at launch), bit 3 = TABLE materials looked up
+// in global memory.  Leaving out what a plan does not use lowers register pressure (f64 staged: 92 VGPRs
+// without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
+// table lookup the surface loop never waits on the vmcnt counter, which on gfx950 would also wait for
+// every history store in flight (see kLdsTablePairs).  rtpb_plan::feat picks the variant.
+template <typename TIN, typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
+__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+void trace_kernel(TraceArgs<TIN, TS> a) {
+    constexpr int kB = trace_block(OUT_LAYOUT, STORE);
+    using T = double;
+    constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
+    constexpr bool kNT = (STORE & 2) != 0;
+    // STORE bit 3: only the final plane is stored (planes='final'): no per-surface store logic, one
+    // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
+    constexpr bool kFinal = (STORE & 8) != 0;
+    constexpr bool kLens = (FEAT & 1) != 0, kPoly = (FEAT & 2) != 0;
+    constexpr bool kTabLds = (FEAT & 12) == 4, kTabGlobal = (FEAT & 8) != 0;
+    extern __shared__ double lds_table[];                // FEAT bit 2: the plan's (wavelength, n) pairs
+    if constexpr (kTabLds) {
+        // before any wave can leave: the unstaged variants run four-wave workgroups and need the barrier
+        for (int k = threadIdx.x; k < 2 * a.ntable; k += kB) lds_table[k] = a.table[k];
+        if constexpr (kB > 64) __syncthreads();
+    }
+    // per wave: "at" and "after" tiles of 64 records (4 KiB f64, 2 KiB f32: the LDS budget allows 5 f64 /
+    // 10 f32 waves per SIMD in the all-planes mode, so registers set the f32 occupancy)
+    __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16 * sizeof(TS) / 8];
+    const int lane = threadIdx.x & 63;
+    // one block of kB rays (the whole kernel, or one step of the persistent experiment's loop)
+    auto body = [&](const int64_t blk) {
+#if defined(RTPB_EXP_XCD_REMAP)             // experiment only: each XCD takes a contiguous range of ray blocks
+    // workgroups are dispatched round-robin over the 8 XCDs: block b runs on XCD b % 8
+    const uint32_t nb = gridDim.x, per = nb / 8, xcd = blockIdx.x % 8, k = blockIdx.x / 8;
+    const uint32_t bid = blockIdx.x < per * 8 ? xcd * per + k : blockIdx.x;
+    const int64_t i = static_cast<int64_t>(bid) * kB + threadIdx.x;
+#elif defined(RTPB_EXP_SCATTER)           // experiment only: ray blocks visited in a scattered order
+    // block b -> (b * RTPB_EXP_SCATTER) mod nb, a bijection when nb is not a multiple of the prime
+    const int64_t nb = gridDim.x;
+    const int64_t bs = (nb % RTPB_EXP_SCATTER) ? (blk * RTPB_EXP_SCATTER) % nb : blk;
+    const int64_t i = bs * kB + threadIdx.x;
+#else
+    const int64_t i = blk * kB + threadIdx.x;
+#endif
+    const int64_t ray0 = i - lane;                       // first ray of this wave
+    if (ray0 >= a.n) return;                             // wave-uniform exit
+#if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
+    // consecutive workgroups go to different XCDs, so the delay step uses blockIdx / 8 (varies inside
+    // an XCD); 0..7 steps of s_sleep(RTPB_EXP_STAGGER) (64 cycles per unit)
+    if (blockIdx.x < 8192)
+        for (unsigned k = 0; k < ((blockIdx.x >> 3) & 7u); ++k) __builtin_amdgcn_s_sleep(RTPB_EXP_STAGGER);
+#endif
+    const bool valid = i < a.n;
+    uint4* tile_a = tiles[threadIdx.x >> 6][0];
+    uint4* tile_b = tiles[threadIdx.x >> 6][kFinal ? 0 : 1];
+    Ray<T> r;
+#if defined(RTPB_EXP_NO_INPUT)             // experiment only: no input reads (write-only memory path)
+    {
+        const T v = T(i);
+        r.x = v; r.y = v; r.z = v; r.dx = v; r.dy = v; r.dz = v; r.ph = v; r.wl = T(0.5);
+    }
+#else
+    // staged input loads use the output tile, so they need the input records to be TS-sized
+    if constexpr (kStaged && IN_LAYOUT == RTPB_AOS && (STORE & 4) && std::is_same<TIN, TS>::value)
+        r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
+    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
+#endif
+    const T wl0 = r.wl;
+    const Rcp<T> iwl = make_rcp(wl0);                    // shared divisor of every phase update
+    TS* __restrict__ out = a.out;
+    const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
+    const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
+    const cptr<T> table = (cptr<T>)(a.table);
+    auto mat_n = [&](cptr<DevMaterial<T>> mp) -> T {
+        if constexpr (kTabLds) return material_n<T, kPoly, true>(load_material<T>(mp), wl0, lds_table);
+        else return material_n<T, kPoly, kTabGlobal>(load_material<T>(mp), wl0, table);
+    };
+    if constexpr (kFinal) {
+        T n_cur = mat_n(mats);
+        for (int s = 0; s < a.nsurf; ++s) {
+            const T n_next = mat_n(mats + s + 1);
+            Ray<T> after;
+            propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
+                                                         [](const Ray<T>&) {}, after);
+            r = after;
+            n_cur = n_next;
+        }
+        if constexpr (kStaged) {
+            tile_write<TS>(tile_b, lane, r);
+            lds_wait();
+            tile_flush<TS, kNT>(tile_b, out, ray0, a.n, lane);
+        } else if (valid) {
+            store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
+        }
+        return;
+    }
+    int64_t slot_off = 0;
+    if (a.mask_lo & 1ull) {
+        if constexpr (kStaged) {
+            tile_write<TS>(tile_a, lane, r);
+            lds_wait();
+            tile_flush<TS, kNT>(tile_a, out, ray0, a.n, lane);
+        } else if (valid) {
+            store_ray<TS, OUT_LAYOUT>(out, i, a.out_fs, r);
+        }
+        slot_off += a.out_ps;
+    }
+    T n_cur = mat_n(mats);
+    for (int s = 0; s < a.nsurf; ++s) {
+        const T n_next = mat_n(mats + s + 1);
+        const int p = 2 * s + 1;
+        const bool st_at = plane_bit(a.mask_lo, a.mask_hi, p);          // wave-uniform
+        const bool st_after = plane_bit(a.mask_lo, a.mask_hi, p + 1);
+        const int64_t off_at = slot_off;
+        slot_off += st_at ? a.out_ps : 0;
+        const int64_t off_after = slot_off;
+        slot_off += st_after ? a.out_ps : 0;
+        // the "at" plane goes to its LDS tile (or straight out) as soon as it is final
+        auto emit_at = [&](const Ray<T>& at) {
+            if constexpr (kStaged) {
+                if (st_at) tile_write<TS>(tile_a, lane, at);
+            } else {
+                if (valid && st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
+            }
+        };
+        Ray<T> after;
+#if defined(RTPB_EXP_NO_COMPUTE)           // experiment only: the kernel's pure memory path
+        after = r;
+        after.ph = r.ph + n_next + n_cur;
+        emit_at(r);
+#else
+        propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
+#endif
+        if constexpr (kStaged) {
+            // both planes of the surface share one LDS round trip
+            if (st_after) tile_write<TS>(tile_b, lane, after);
+            if (st_at || st_after) lds_wait();
+            if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
+            if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
+        } else if (valid) {
+            if (st_after) store_ray<TS, OUT_LAYOUT>(out + off_after, i, a.out_fs, after);
+        }
+        r = after;
+        n_cur = n_next;
+    }
+    };
+#if defined(RTPB_EXP_PERSIST)              // experiment only: persistent grid, block-stride loop
+    for (int64_t blk = blockIdx.x; blk * kB < a.n; blk += gridDim.x) body(blk);
+#else
+    body(static_cast<int64_t>(blockIdx.x));
+#endif
+}
+
+
+
+template <typename TI, typename T, int IL, int OL, int ST, int W, int FEAT>
+hipError_t launch_w(const TraceArgs<TI, T>& a, hipStream_t st) {
+    constexpr int kB = trace_block(OL, ST);
+    const int64_t blocks = (a.n + kB - 1) / kB;
+    const size_t lds = (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
+#if defined(RTPB_EXP_PERSIST)
+    static int resident = 0;                     // experiment: one wave slot per workgroup of the grid
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<TI, T, IL, OL, ST, W, FEAT>, kB, lds);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        resident = per_cu * cus * RTPB_EXP_PERSIST;
+    }
+    const int64_t grid = blocks < resident ? blocks : resident;
+#else
+    const int64_t grid = blocks;
+#endif
+    hipLaunchKernelGGL((trace_kernel<TI, T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(grid)), dim3(kB), lds,
+                       st, a);
+    return hipGetLastError();
+}
+
+template <typename TI, typename T, int IL, int OL, int ST>
+hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
+    if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
+        const int w = g_waves_per_eu.load();
+        if (w == 5) return launch_w<TI, T, IL, OL, ST, 5, 15>(a, st);
+    }
+#if defined(RTPB_EXP_WPE)                  // experiment only: minimum waves per SIMD for every variant
+    constexpr int kW = RTPB_EXP_WPE;
+#else
+    constexpr int kW = 1;
+#endif
+    switch (feat) {
+    case 0: return launch_w<TI, T, IL, OL, ST, kW, 0>(a, st);
+    case 1: return launch_w<TI, T, IL, OL, ST, kW, 1>(a, st);
+    case 4: return launch_w<TI, T, IL, OL, ST, kW, 4>(a, st);
+    case 5: return launch_w<TI, T, IL, OL, ST, kW, 5>(a, st);
+    default: return launch_w<TI, T, IL, OL, ST, kW, 15>(a, st);    // POLY6 or a large table: everything in
+    }
+}
+
+template <typename TI, typename T>
+hipError_t launch_trace(const TraceArgs<TI, T>& a, int il, int ol, int feat, hipStream_t st) {
+    const bool staged = g_aos_staging.load() != 0;
+    const bool nt = g_nt_stores.load() != 0;
+    const int last = 2 * a.nsurf;                       // planes='final': only the last plane stored
+    const bool final_only = a.nsurf > 0 && (last < 64 ? (a.mask_lo == (1ull << last) && a.mask_hi == 0)
+                                                      : (a.mask_lo == 0 && a.mask_hi == (1ull << (last - 64))));
+    if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load() &&
+        g_waves_per_eu.load() == 0)
+        return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 11>(a, feat, st);
+    if constexpr (!std::is_same<TI, T>::value) {
+        // input and storage types differ: AOS input only (rtpb_trace checks), no staged-input variant
+        if (ol == RTPB_SOA) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
+        if (!staged) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st);
+        return nt ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st);
+    }
+    if (ol == RTPB_AOS) {
+        if (!staged)
+            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 0>(a, feat, st);
+        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 7>(a, feat, st);
+        if (nt)
+            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 3>(a, feat, st);
+        return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 1>(a, feat, st);
+    }
+    if (il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
+    return launch_one<TI, T, RTPB_SOA, RTPB_SOA, 0>(a, feat, st);
+}
+
+
+}  // namespace rtpbi

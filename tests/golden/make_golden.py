@@ -34,13 +34,18 @@ def _child():
     meta = {"numpy": np.__version__, "reference": "QI2lab/ray_trace_pb @ 2024_10_08"}
 
     only = [v for v in os.environ.get("RTPB_GOLDEN_ONLY", "").split(",") if v]
-    for name, recipe in systems.RECIPES.items():
+    # float32 INPUT variants (<recipe>_f32in): the reference run on the recipe's rays rounded to
+    # float32, i.e. what a caller handing it float32 arrays gets back (a float64 history)
+    recipes = [(n, r, False) for n, r in systems.RECIPES.items()]
+    recipes += [(n + "_f32in", systems.RECIPES[n], True) for n in systems.F32_INPUT_CASES]
+    for name, recipe, f32in in recipes:
         if only and name not in only:
             continue
         system, rays, m_init, m_final = recipe(rt, mat)
+        rays = np.asarray(rays, dtype=np.float32 if f32in else np.float64)
         hist = system.ray_trace(rays, m_init, m_final)
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"),
-                            rays_in=np.asarray(rays, dtype=np.float64),
+                            rays_in=rays,
                             history=np.asarray(hist, dtype=np.float64),
                             system_json=np.array(system_to_json(system, m_init, m_final)),
                             meta_json=np.array(json.dumps(meta)))

@@ -433,3 +433,7 @@ RECIPES = {
     "lightsheet_r120": lambda rt, mat: lightsheet(rt, mat, 120.0),
     "lightsheet_r1e9": lambda rt, mat: lightsheet(rt, mat, 1e9),
 }
+
+# recipes also recorded with their input rays rounded to float32 (<name>_f32in.npz): the reference's
+# answer for float32 input, which the float32-input paths must reproduce
+F32_INPUT_CASES = ("c2_achromat", "c3_relay", "c4_opm", "c5_odt", "stress")

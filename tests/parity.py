@@ -6,8 +6,12 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
-               if os.path.basename(f)[:-4] not in ("shapes", "generators"))
+ALL_CASES = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                   if os.path.basename(f)[:-4] not in ("shapes", "generators"))
+# float64-input recipes (the reference run on float64 rays) and their float32-input variants (the same
+# recipe's rays rounded to float32 and handed to the reference as float32 arrays)
+CASES = [c for c in ALL_CASES if not c.endswith("_f32in")]
+F32IN_CASES = [c for c in ALL_CASES if c.endswith("_f32in")]
 
 
 def load_case(name):
@@ -30,7 +34,8 @@ def compare(got, ref, rtol):
     absref = np.where(np.isfinite(ref), np.abs(ref), 0.0)
     colmax = absref.max(axis=-2, keepdims=True) if ref.ndim >= 2 else absref.max()
     scale = np.maximum(absref, colmax)
-    err = np.where(fin, np.abs(got - ref), 0.0)
+    with np.errstate(invalid="ignore"):
+        err = np.where(fin & (got != ref), np.abs(got - ref), 0.0)      # equal infinities: no error
     inf_mismatch = int((fin & (np.isinf(got) | np.isinf(ref)) & (got != ref)).sum())
     err = np.where(np.isinf(err), 0.0, err)
     with np.errstate(invalid="ignore", divide="ignore"):

@@ -85,9 +85,9 @@ def test_trace_without_gpu_fails_loudly():
     assert lib.rtpb_plan_create(surf, 1, mats, 2, C.RTPB_F64, ctypes.byref(plan)) == 0
     rays = np.zeros((4, 8))
     out = np.zeros((3, 4, 8))
-    rc = lib.rtpb_trace_host(plan, rays.ctypes.data, 4, out.ctypes.data, 7, 0, None, 0)
+    rc = lib.rtpb_trace_host(plan, rays.ctypes.data, 0, 4, out.ctypes.data, 7, 0, None, 0)
     assert rc == -3 and b"no GPU" in lib.rtpb_last_error()
-    rc = lib.rtpb_trace(plan, 0, rays.ctypes.data, 4, 0, 0, out.ctypes.data, 0, 32, 0, 7, 0, None)
+    rc = lib.rtpb_trace(plan, 0, rays.ctypes.data, 0, 4, 0, 0, out.ctypes.data, 0, 32, 0, 7, 0, None)
     assert rc == -3
     lib.rtpb_plan_destroy(plan)
 

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 from oracle import rt_numpy as O
-from parity import CASES, load_case
+from parity import CASES, F32IN_CASES, compare, load_case
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -12,6 +12,20 @@ def test_oracle_matches_reference_bitwise(name):
     got = O.ray_trace(spec["surfaces"], spec["materials"], rays)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref, equal_nan=True)
+
+
+@pytest.mark.parametrize("name", F32IN_CASES)
+def test_oracle_on_widened_float32_input_vs_reference(name):
+    """The reference given float32 rays returns a float64 history.  NumPy's promotion rules make it
+    evaluate a few first-surface sub-expressions in float32 (``2 * np.pi / wls`` in PerfectLens RT:1773,
+    ``wavelength ** 2`` in Sellmeier MAT:48-50); every later surface sees the float64 history.  The
+    oracle (and the GPU) widen the float32 input exactly and compute everything in float64: NaN masks
+    must be identical and values within 1e-6 column-scaled (float32 bar: 1e-5)."""
+    spec, rays, ref = load_case(name)
+    assert rays.dtype == np.float32 and ref.dtype == np.float64
+    got = O.ray_trace(spec["surfaces"], spec["materials"], rays.astype(np.float64))
+    ok, rep = compare(got, ref, rtol=1e-6)
+    assert ok and rep["mask_flips"] == 0, rep
 
 
 def test_oracle_input_ranks():

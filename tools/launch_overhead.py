@@ -34,7 +34,7 @@ def main(steps=400):
     n = x.shape[0]
 
     def raw(stream):
-        C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), n, C.RTPB_AOS, 0, out.data_ptr(), C.RTPB_AOS, 8 * n, n,
+        C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), E.input_code(x.dtype), n, C.RTPB_AOS, 0, out.data_ptr(), C.RTPB_AOS, 8 * n, n,
                                lo, hi, stream))
 
     def wall(fn, k):

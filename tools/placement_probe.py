@@ -86,7 +86,7 @@ def main():
         def run(lib, ptr):
             C._lib, E._PLANS = lib, caches[[k for k in libs if libs[k] is lib][0]]
             with E.plan_ref(low) as plan:
-                C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), x.shape[0], C.RTPB_AOS, 0, ptr, C.RTPB_AOS,
+                C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), E.input_code(x.dtype), x.shape[0], C.RTPB_AOS, 0, ptr, C.RTPB_AOS,
                                        8 * x.shape[0], x.shape[0], lo, hi, torch.cuda.current_stream().cuda_stream))
         tun = {ln: (None, None) for ln in libs}
         for t in filter(None, args.tunings.split(",")):
