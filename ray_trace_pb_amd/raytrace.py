@@ -46,7 +46,7 @@ def get_free_space_abcd(d: float, n: float = 1.) -> np.ndarray:
 
 # =============================================================================== ray generators
 def get_ray_fan(pt, theta_max: float, n_thetas: int, wavelengths, nphis: int = 1, center_ray=(0, 0, 1),
-                *, device=None, dtype=None):
+                *, device=None, dtype=None, devices=None):
     """Fan of rays leaving the point ``pt`` (RT:45-96).
 
     Ray (iphi, itheta) -> index iphi*n_thetas + itheta; direction
@@ -54,10 +54,21 @@ def get_ray_fan(pt, theta_max: float, n_thetas: int, wavelengths, nphis: int = 1
     theta in linspace(-theta_max, theta_max, n_thetas), phi = k 2 pi / nphis.  Phase 0.
 
     With ``device`` (a torch CUDA device), the fan is generated directly in HBM by the ``rtpb_ray_fan_tables``
-    kernel and returned as a torch tensor (``wavelengths`` must then be a scalar)."""
+    kernel and returned as a torch tensor (``wavelengths`` must then be a scalar).  With ``devices`` (GPU
+    indices) it is generated as contiguous ray-index shards, one per GPU (whole phi rows, as even as the
+    row count allows), and returned as the list of per-device tensors -- the input of a multi-GPU
+    ``System.ray_trace`` that never gathers (e.g. the C4 configuration, 100M rays over 8 GPUs)."""
     center_ray = np.array(center_ray)
     if np.linalg.norm(center_ray) != 1:
         raise ValueError("center_ray must be a unit vector")
+    if devices is not None:
+        import torch
+        out = []
+        for (p0, p1), d in zip(shard_bounds(int(nphis), len(devices)), devices):
+            buf = torch.empty(((p1 - p0) * n_thetas, 8), device=torch.device("cuda", int(d)),
+                              dtype=torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64)
+            out.append(fan_into(buf, pt, theta_max, n_thetas, wavelengths, nphis, center_ray, phi_rows=(p0, p1)))
+        return out
     if device is not None:
         return _ray_fan_device(pt, theta_max, n_thetas, wavelengths, nphis, center_ray, device, dtype)
     thetas = np.linspace(-theta_max, theta_max, n_thetas)
@@ -101,9 +112,11 @@ def _fan_tables(theta_max, n_thetas, nphis, center_ray, center_dtype):
     return enx, eny, tcs, pcs
 
 
-def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0, 1)):
+def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0, 1), phi_rows=None):
     """Write get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray) into the torch CUDA
-    buffer ``buf`` ((n_thetas*nphis, 8), float64 or float32) on its current stream.
+    buffer ``buf`` ((n_thetas*nphis, 8), float64 or float32) on its current stream.  ``phi_rows=(p0, p1)``
+    writes only rays p0*n_thetas .. p1*n_thetas - 1 (a contiguous shard; ``buf`` then has
+    (p1-p0)*n_thetas rows).
 
     Every host-side value of RT:71-81 -- the linspace thetas, the phis, their np.cos / np.sin, and the
     enx / eny basis -- is evaluated here with NumPy exactly as the reference does (n_thetas + nphis
@@ -115,8 +128,14 @@ def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0
                                      center_ray.dtype.str)
     vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (pt, center_ray, enx, eny)]
     code = C.RTPB_F64 if buf.dtype == torch.float64 else C.RTPB_F32
+    p0, p1 = (0, int(nphis)) if phi_rows is None else (int(phi_rows[0]), int(phi_rows[1]))
+    if not 0 <= p0 <= p1 <= nphis or buf.shape != (int(n_thetas) * (p1 - p0), 8) or not buf.is_contiguous():
+        raise ValueError("fan_into: buffer shape does not match the fan (or its phi rows)")
+    if p1 == p0:
+        return buf
+    pcs = np.ascontiguousarray(pcs[p0:p1])
     C.check(C.lib().rtpb_ray_fan_tables(buf.device.index or 0, code, buf.data_ptr(), vec[0].ctypes.data,
-                                        int(n_thetas), int(nphis), vec[1].ctypes.data, vec[2].ctypes.data,
+                                        int(n_thetas), p1 - p0, vec[1].ctypes.data, vec[2].ctypes.data,
                                         vec[3].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, float(wavelength),
                                         torch.cuda.current_stream(buf.device).cuda_stream))
     return buf
@@ -316,18 +335,45 @@ def _dtype_code(dtype, rays):
     raise ValueError(f"dtype must be float64 or float32, got {dtype!r}")
 
 
-def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devices=None, layout="aos"):
+def _is_shard_list(rays):
+    return isinstance(rays, (list, tuple)) and len(rays) > 0 and all(_is_torch_cuda(r) for r in rays)
+
+
+def shard_bounds(n, n_shards):
+    """Contiguous ray-index shards [lo, hi) of n rays over n_shards devices -- the split rtpb_trace_host and
+    ray_trace_pb_amd.distributed use."""
+    return [(n * g // n_shards, n * (g + 1) // n_shards) for g in range(n_shards)]
+
+
+def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devices=None, layout="aos", gather=True):
     """Trace ``rays`` through ``surfaces`` with ``materials`` (len(surfaces)+1 entries) on the GPU.
 
     ``rays`` follows the reference's rank convention (RT:1175-1178): (8,) -> one ray, (N, 8) -> a
     bundle (history plane 0 = the input), (k, N, 8) -> an existing history whose last plane is traced
     and which is extended.  ``planes`` = 'all' (reference output), 'final', or a list of plane indices
-    of the new trace (0 = input, 2i+1 at surface i, 2i+2 after it)."""
+    of the new trace (0 = input, 2i+1 at surface i, 2i+2 after it).
+
+    Multi-GPU in one process: a NumPy bundle with ``devices`` is split by ray index inside the library
+    (one host thread per GPU); a torch CUDA bundle with ``devices`` is scattered by ray index to the
+    listed GPUs, traced there concurrently, and gathered back onto its own device (``gather=False``:
+    the list of per-device histories instead); a list of torch CUDA shards (one per device, e.g. from
+    ``get_ray_fan(..., devices=)``) is traced where it lives and returns the list of per-device
+    histories.  Systems longer than RTPB_MAX_SURFACES run as consecutive fused segments."""
     if len(materials) != len(surfaces) + 1:
         raise ValueError("length of materials should be len(surfaces) + 1")
     if not surfaces:
         return rays
+    if _is_shard_list(rays):
+        # each shard on its own device: launches are asynchronous, so the devices trace concurrently
+        return [trace_surfaces(surfaces, materials, r, planes=planes, dtype=dtype, layout=layout) for r in rays]
     on_device = _is_torch_cuda(rays)
+    if on_device and devices is not None:
+        devs = _resolve_devices(devices)
+        if devs and (len(devs) > 1 or devs[0] != rays.device.index):
+            return _trace_scattered(surfaces, materials, rays, devs, planes=planes, dtype=dtype, layout=layout,
+                                    gather=gather)
+    if len(surfaces) > C.RTPB_MAX_SURFACES:
+        return _trace_segmented(surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices, layout=layout)
     if not on_device:
         rays = np.asarray(rays)
     if rays.ndim == 1:
@@ -363,6 +409,85 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
         E.trace_host(low, last, sel[1:], devs, out=out[k:])
         return out
     return E.trace_host(low, last, sel, devs)
+
+
+def _trace_scattered(surfaces, materials, rays, devs, *, planes, dtype, layout, gather):
+    """A torch CUDA bundle split by ray index over ``devs``: each shard is copied to its
+    GPU (device-to-device), traced there on that device's current stream, and -- with ``gather`` --
+    copied back into one history on the bundle's own device.  Rays are independent, so the result is
+    bit-identical to a single-device trace."""
+    import torch
+    if rays.ndim == 1:
+        rays = rays[None, None, :]
+    elif rays.ndim == 2:
+        rays = rays[None]
+    n = rays.shape[1]
+    shards = []
+    for (a, b), d in zip(shard_bounds(n, len(devs)), devs):
+        dev = torch.device("cuda", d)
+        shards.append(rays[:, a:b] if dev == rays.device else rays[:, a:b].to(dev, non_blocking=True))
+    outs = [trace_surfaces(surfaces, materials, r if r.shape[0] > 1 else r[0], planes=planes, dtype=dtype,
+                           layout=layout) for r in shards]
+    if not gather:
+        return outs
+    axis = 2 if layout == "soa" else 1
+    shape = list(outs[0].shape)
+    shape[axis] = n
+    out = torch.empty(shape, dtype=outs[0].dtype, device=rays.device)
+    for (a, b), o in zip(shard_bounds(n, len(devs)), outs):
+        out.narrow(axis, a, b - a).copy_(o, non_blocking=True)
+    return out
+
+
+def _trace_segmented(surfaces, materials, rays, *, planes, dtype, devices, layout):
+    """A system longer than RTPB_MAX_SURFACES (the 128-bit plane mask of one fused launch) runs as
+    consecutive fused segments of at most RTPB_MAX_SURFACES surfaces, each continuing from the previous
+    segment's last plane exactly as the reference's surface loop continues (RT:658-659, 3-D histories
+    RT:1175-1178).  Segments are traced with float64 storage -- the continuation must not be rounded --
+    and the requested planes are assembled (and rounded once, for float32 storage) at the end."""
+    on_device = _is_torch_cuda(rays)
+    if on_device:
+        import torch
+        xp_stack, xp_cat = torch.stack, torch.cat
+    else:
+        rays = np.asarray(rays)
+        xp_stack, xp_cat = np.stack, np.concatenate
+    if rays.ndim == 1:
+        rays = rays[None, None, :]
+    elif rays.ndim == 2:
+        rays = rays[None]
+    if rays.ndim != 3 or rays.shape[-1] != 8:
+        raise ValueError(f"rays must have shape (8,), (N, 8) or (k, N, 8); got {tuple(rays.shape)}")
+    S = len(surfaces)
+    code = _dtype_code(dtype, rays)
+    sel = E.resolve_planes(planes, S)
+    want = set(sel)
+    full = isinstance(planes, str) and planes == "all"
+    pieces = {}
+    cur = rays[-1]
+    if 0 in want:
+        pieces[0] = cur.double() if on_device else np.asarray(cur, dtype=np.float64)
+    M = C.RTPB_MAX_SURFACES
+    for s0 in range(0, S, M):
+        s1 = min(S, s0 + M)
+        last = 2 * (s1 - s0)
+        req = sorted({p - 2 * s0 for p in want if 2 * s0 < p <= 2 * s1} | {last})
+        res = trace_surfaces(surfaces[s0:s1], materials[s0:s1 + 1], cur, planes=req, dtype="float64", devices=devices)
+        for p, arr in zip(req, res):
+            if 2 * s0 + p in want:
+                pieces[2 * s0 + p] = arr
+        cur = res[-1]
+    out = xp_stack([pieces[p] for p in sel])
+    if code == C.RTPB_F32:
+        out = out.float() if on_device else out.astype(np.float32)
+    if full and rays.shape[0] > 1:
+        head = rays.to(out.dtype) if on_device else rays.astype(out.dtype)
+        out = xp_cat((head, out[1:]))
+    if layout == "soa":
+        if not on_device:
+            raise ValueError("layout='soa' is only available for device (torch CUDA) inputs")
+        out = out.transpose(1, 2).contiguous()
+    return out
 
 
 def _resolve_devices(devices):
@@ -530,26 +655,34 @@ class System:
 
     # ------------------------------------------------------------------ the hot path (RT:641-661)
     def ray_trace(self, rays, initial_material: Material, final_material: Material, *, planes="all",
-                  dtype=None, devices=None, layout="aos"):
+                  dtype=None, devices=None, layout="aos", gather=True):
         """Trace rays through the system; returns the ray history.
 
         Same contract as the reference: (N, 8) rays -> (2S+1, N, 8) history (plane 0 = input, plane
         2i+1 at surface i, 2i+2 after it), (8,) -> (2S+1, 1, 8), (k, N, 8) -> (k+2S, N, 8).  Computed in
-        float64 on the GPU by one fused kernel.  Keyword-only extensions:
+        float64 on the GPU by one fused kernel (systems longer than RTPB_MAX_SURFACES = 63 surfaces by
+        consecutive fused segments).  Keyword-only extensions:
 
         planes   'all' (default) | 'final' | list of plane indices -- store only what is needed
-        dtype    None/float64 (reference numerics) | float32
-        devices  None (GPU 0) | 'all' | list of GPU indices to shard NumPy bundles over
+        dtype    None/float64 (reference numerics) | float32 storage of the history (float64 arithmetic;
+                 float64 rays are not rounded before the trace)
+        devices  None (the bundle's GPU / GPU 0) | 'all' | list of GPU indices: ray-index shards, one per
+                 GPU, traced concurrently (NumPy: host threads in the library; torch: device-to-device
+                 scatter and gather)
         layout   'aos' (default) | 'soa' (torch inputs only: (planes, 8, N) output)
+        gather   torch input with devices: False returns the list of per-device histories (no gather)
 
-        torch CUDA tensors in -> torch CUDA tensors out (nothing leaves HBM)."""
+        torch CUDA tensors in -> torch CUDA tensors out (nothing leaves HBM); a list of per-device torch
+        shards (e.g. ``get_ray_fan(..., devices=...)``) -> the list of per-device histories."""
         materials = [initial_material] + list(self.materials) + [final_material]
         if len(materials) != len(self.surfaces) + 1:
             raise ValueError("length of materials should be len(surfaces) + 1")
         custom = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
-                                  layout=layout)
+                                  layout=layout, gather=gather)
+        if _is_shard_list(rays):
+            return [self.ray_trace(r, initial_material, final_material, dtype=dtype) for r in rays]
         # user surfaces (own propagate, or own geometry hooks): run maximal runs of built-in surfaces
         # as fused GPU traces and hand the growing history to each user surface in between
         # (RT:658-659 order)

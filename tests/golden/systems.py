@@ -437,3 +437,39 @@ RECIPES = {
 # recipes also recorded with their input rays rounded to float32 (<name>_f32in.npz): the reference's
 # answer for float32 input, which the float32-input paths must reproduce
 F32_INPUT_CASES = ("c2_achromat", "c3_relay", "c4_opm", "c5_odt", "stress")
+
+
+# ------------------------------------------------------------------ long systems (> RTPB_MAX_SURFACES)
+def long_system(rt, mat, n_lenses=49):
+    """A train of weak Bk7 / N-SF11 biconvex lenses (2 spheres each) with a pupil flat after every tenth
+    lens, a PerfectLens in the middle and a final image flat: 2 * n_lenses + n_lenses // 10 + 2 surfaces
+    (49 lenses: 104 surfaces, 209 history planes) -- beyond one fused launch's 63 surfaces."""
+    surfaces, materials = [], []
+    z = 0.0
+    for k in range(n_lenses):
+        glass = mat.Bk7() if k % 2 == 0 else mat.Nsf11()
+        surfaces.append(rt.SphericalSurface.get_on_axis(400.0, z, 12.0))
+        surfaces.append(rt.SphericalSurface.get_on_axis(-400.0, z + 2.0, 12.0))
+        materials += [glass, mat.Vacuum()]
+        z += 6.0
+        if k % 10 == 9:
+            surfaces.append(rt.FlatSurface([0, 0, z - 2.0], [0, 0, 1], 4.0))
+            materials.append(mat.Vacuum())
+        if k == n_lenses // 2:
+            surfaces.append(rt.PerfectLens(50.0, [0, 0, z - 1.0], [0, 0, 1], 0.6))
+            materials.append(mat.Vacuum())
+    surfaces.append(rt.FlatSurface([0, 0, z + 5.0], [0, 0, 1], 30.0))
+    return rt.System(surfaces, materials)
+
+
+def long_rays(nrays=2000, seed=SEED + 3):
+    """Collimated rays in a 6 mm disk at three wavelengths, a few tilted."""
+    rng = np.random.default_rng(seed)
+    r = 6.0 * np.sqrt(rng.uniform(0, 1, nrays))
+    a = rng.uniform(0, 2 * np.pi, nrays)
+    rays = np.zeros((nrays, 8))
+    rays[:, 0], rays[:, 1], rays[:, 2] = r * np.cos(a), r * np.sin(a), -5.0
+    d = np.stack((rng.normal(scale=0.01, size=nrays), rng.normal(scale=0.01, size=nrays), np.ones(nrays)), axis=1)
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1)[:, None]
+    rays[:, 7] = np.array([0.486, 0.5876, 0.6563])[np.arange(nrays) % 3]
+    return rays

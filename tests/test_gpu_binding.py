@@ -1,0 +1,78 @@
+"""GPU: the reference-side ctypes binding of INTEGRATION.md §3 (tests/reference_binding.py) -- what a
+maintainer of the reference would add -- run against the reference's golden histories.  It talks to
+librtpb.so through the C ABI alone; the systems are this repository's drop-in objects, which carry the
+reference's class names and attributes."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from ray_trace_pb_amd import _capi as C  # noqa: E402
+from oracle import rt_numpy as O  # noqa: E402
+from parity import CASES, GOLDEN  # noqa: E402
+from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
+import reference_binding  # noqa: E402
+import systems  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ray_trace_gpu():
+    C.lib()                                           # torch's HIP runtime first (see _capi.lib)
+    return reference_binding.make_ray_trace(rt, mat, C.LIB_PATH)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_binding_reproduces_reference_histories(ray_trace_gpu, name):
+    d = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    got = ray_trace_gpu(system, d["rays_in"], m0, m1)
+    assert got.dtype == np.float64 and got.shape == d["history"].shape
+    assert np.array_equal(got, d["history"], equal_nan=True)
+
+
+def test_binding_input_ranks_and_history_extension(ray_trace_gpu):
+    d = np.load(os.path.join(GOLDEN, "shapes.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    for k in ("1", "2", "3"):
+        got = ray_trace_gpu(system, d["rays" + k], m0, m1)
+        assert got.shape == d["out" + k].shape and np.array_equal(got, d["out" + k], equal_nan=True), k
+
+
+def test_binding_surface_and_material_subclasses(ray_trace_gpu):
+    """A FlatSurface subclass without own geometry lowers as a flat; one with its own get_intersect makes
+    the call fall back to the reference's Python loop; a user Material subclass lowers to a table."""
+    d = np.load(os.path.join(GOLDEN, "stress.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    assert any(type(m).__name__ == "Cauchy" for m in system.materials)
+
+    class TaggedFlat(rt.FlatSurface):
+        tag = "pupil"
+
+    class HookedFlat(rt.FlatSurface):
+        def get_intersect(self, rays, material):
+            return super().get_intersect(rays, material)
+
+    for cls in (TaggedFlat, HookedFlat):
+        surfs = [cls(s.center, s.normal, s.aperture_rad) if type(s) is rt.FlatSurface else s
+                 for s in system.surfaces]
+        kinds = [reference_binding._builtin_kind(rt, s) for s in surfs]
+        assert (None in kinds) == (cls is HookedFlat)
+        got = ray_trace_gpu(rt.System(surfs, system.materials), d["rays_in"], m0, m1)
+        assert np.array_equal(got, d["history"], equal_nan=True), cls.__name__
+
+
+def test_binding_chains_launches_beyond_63_surfaces(ray_trace_gpu):
+    system = systems.long_system(rt, mat)
+    rays = systems.long_rays(1500)
+    m0, m1 = mat.Vacuum(), mat.Vacuum()
+    ref = O.ray_trace([surface_to_dict(s) for s in system.surfaces],
+                      [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]], rays)
+    got = ray_trace_gpu(system, rays, m0, m1)
+    assert got.shape == ref.shape and np.array_equal(got, ref, equal_nan=True)

@@ -57,3 +57,71 @@ def test_round_trip_device_histories(tmp_path):
     got = read_array(p)
     for i in range(3):
         assert np.array_equal(got[i], ref[i], equal_nan=True)
+
+
+LIGHTSHEET_RADII = (8.0, 120.0, 1e9)
+# scripts/2024_04_01_lightsheet.py:23-36 (the script's settings dict, stored as the store's attrs)
+LIGHTSHEET_SETTINGS = {"nrays": 1001, "wavelength": 0.532, "aperture_radius_etl": 8, "aperture_radius": 50.8 / 2,
+                       "n_etl": 1.3, "t_edge": 5, "f1": 160, "f2": 120, "fobj": 20, "t_coverglass": 1.25,
+                       "n_coverglass": 1.4585, "dz_coverglass": 10, "n_immersion": 1.333}
+
+
+def _lightsheet_golden(r):
+    from parity import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "lightsheet_r%s.npz" % {8.0: "8", 120.0: "120", 1e9: "1e9"}[r]))
+    return d["rays_in"], d["history"], str(d["system_json"])
+
+
+def _check_lightsheet_store(p, histories):
+    meta = json.load(open(os.path.join(p, "rays", ".zarray")))
+    # the script's z.create("rays", shape=(n_config, 17, nrays, 8), chunks=(1, 17, nrays, 8), dtype=float)
+    assert meta["shape"] == [3, 17, 1001, 8] and meta["chunks"] == [1, 17, 1001, 8] and meta["dtype"] == "<f8"
+    assert read_attrs(p, "rays")["array_columns"] == ["x", "y", "z", "dx", "dy", "dz", "phase", "wavelength"]
+    assert read_attrs(p)["settings"] == LIGHTSHEET_SETTINGS
+    rc = read_array(p, "radius_curvatures")
+    assert np.array_equal(rc, np.array(LIGHTSHEET_RADII))
+    assert np.array_equal(read_array(p, "focal_lens_mm"), rc / (LIGHTSHEET_SETTINGS["n_etl"] - 1))
+    got = read_array(p)
+    for i, h in enumerate(histories):
+        assert np.array_equal(got[i], h, equal_nan=True), i
+
+
+def _write_lightsheet_store(p, histories):
+    rc = np.array(LIGHTSHEET_RADII)
+    focal = rc / (LIGHTSHEET_SETTINGS["n_etl"] - 1)
+    with HistoryWriter(p, len(rc), 17, 1001, attrs={"settings": LIGHTSHEET_SETTINGS}) as w:
+        w.write_array("radius_curvatures", rc)
+        w.write_array("etl_diopters", 1e3 / focal)
+        w.write_array("focal_lens_mm", focal)
+        for i, h in enumerate(histories):
+            w.write(i, h)
+
+
+def test_lightsheet_store_layout_from_reference_histories(tmp_path):
+    """The reference's own lightsheet histories (golden vectors of the script's system at three ETL radii)
+    stored in the script's layout and read back bit for bit."""
+    hist = [_lightsheet_golden(r)[1] for r in LIGHTSHEET_RADII]
+    _write_lightsheet_store(tmp_path / "ref.zarr", hist)
+    _check_lightsheet_store(tmp_path / "ref.zarr", hist)
+
+
+@pytest.mark.gpu
+def test_lightsheet_sweep_traced_on_gpu_and_streamed_matches_reference(tmp_path):
+    """scripts/2024_04_01_lightsheet.py:51-60,134-135 on the GPU: the three golden ETL systems, rebuilt with
+    the drop-in API, traced as device histories and streamed through HistoryWriter (pinned async D2H +
+    writer thread) into one 3-configuration store; the read-back equals the REFERENCE's histories."""
+    torch = pytest.importorskip("torch")
+    import ray_trace_pb_amd.materials as mat
+    import ray_trace_pb_amd.raytrace as rt
+    import systems
+    from serialize import system_to_json
+    dev_hist, ref_hist = [], []
+    for r in LIGHTSHEET_RADII:
+        rays, ref, sys_json = _lightsheet_golden(r)
+        system, rays_rec, m0, m1 = systems.lightsheet(rt, mat, r)
+        assert json.loads(system_to_json(system, m0, m1)) == json.loads(sys_json)
+        assert np.array_equal(rays_rec, rays)
+        dev_hist.append(system.ray_trace(torch.from_numpy(rays).cuda(), m0, m1))
+        ref_hist.append(ref)
+    _write_lightsheet_store(tmp_path / "gpu.zarr", dev_hist)
+    _check_lightsheet_store(tmp_path / "gpu.zarr", ref_hist)
