@@ -51,15 +51,17 @@ def spot_stats(plane, group_size):
 
 
 def spot_sweep(system, initial_material, final_material, field_points, wavelengths, theta_max, n_thetas, nphis=1,
-               center_ray=(0, 0, 1), device="cuda:0", dtype="float64", groups_per_batch=None, fused=True):
+               center_ray=(0, 0, 1), device="cuda:0", dtype="float64", groups_per_batch=None, fused=True,
+               devices=None):
     """Spot diagrams for every (field point, wavelength): a ``get_ray_fan(field, theta_max, n_thetas,
     wavelength, nphis)`` bundle per group, generated, traced (final plane only) and reduced on the GPU.
 
     ``fused=True`` (default) runs generation, trace and reduction as ONE kernel per batch of groups
     (``rtpb_spot_sweep``: no rays touch HBM); ``fused=False`` runs the three steps separately through
     HBM buffers (``rtpb_ray_fan_tables`` -> ``rtpb_trace`` planes='final' -> ``rtpb_spot_stats``).  Both
-    give bit-identical statistics.  Returns (summary dict with arrays shaped (n_fields, n_wavelengths,
-    ...), timing dict)."""
+    give bit-identical statistics.  ``devices`` (fused only): the (field, wavelength) groups are split into
+    contiguous ranges, one per GPU, swept concurrently from this thread (per-device kernel times in the
+    timing dict).  Returns (summary dict with arrays shaped (n_fields, n_wavelengths, ...), timing dict)."""
     import torch
     dev = torch.device(device)
     tdt = torch.float64 if dtype in ("float64", np.float64) else torch.float32
@@ -74,8 +76,11 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
     low = E.lower(system.surfaces, mats, lambda: np.unique(wavelengths), code)
     S = len(system.surfaces)
     if fused:
-        return _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, dev,
+        devs = [dev] if devices is None else [torch.device("cuda", int(d)) for d in devices]
+        return _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, devs,
                                  groups_per_batch)
+    if devices is not None:
+        raise ValueError("devices= needs the fused sweep")
     if groups_per_batch is None:
         groups_per_batch = max(1, min(G, (1 << 27) // per))     # ~128M rays in flight
     sel = E.resolve_planes("final", len(system.surfaces))
@@ -99,10 +104,10 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
     return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt}
 
 
-def _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, dev,
+def _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, nphis, center_ray, devs,
                       groups_per_batch):
     import torch
-    from .raytrace import _fan_tables
+    from .raytrace import _fan_tables, shard_bounds
     c = np.array(center_ray)
     enx, eny, tcs, pcs = _fan_tables(float(theta_max), int(n_thetas), int(nphis), tuple(c.tolist()), c.dtype.str)
     nf, nw = field_points.shape[0], wavelengths.size
@@ -114,24 +119,48 @@ def _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, np
     tiles = -(-per // 256)
     if groups_per_batch is None:
         groups_per_batch = max(1, min(G, 65535, (1 << 26) // (tiles * 7)))   # workspace <= 512 MB
-    ws = torch.empty(groups_per_batch * tiles * 7, dtype=torch.float64, device=dev)
-    stats = torch.empty((G, 7), dtype=torch.float64, device=dev)
     vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (c, enx, eny)]
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    torch.cuda.synchronize(dev)
+    # one contiguous range of groups per device; per device: workspace, statistics, its current stream
+    work = []
+    for (g0, g1), dev in zip(shard_bounds(G, len(devs)), devs):
+        ws = torch.empty(groups_per_batch * tiles * 7, dtype=torch.float64, device=dev)
+        stats = torch.empty((max(g1 - g0, 1), 7), dtype=torch.float64, device=dev)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        work.append((dev, g0, g1, ws, stats, ev, torch.cuda.current_stream(dev)))
+    for dev in devs:
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     with E.plan_ref(low) as plan:
-        for b0 in range(0, G, groups_per_batch):
-            b1 = min(G, b0 + groups_per_batch)
-            gp = np.ascontiguousarray(params[b0:b1])
-            C.check(C.lib().rtpb_spot_sweep(plan, dev.index or 0, b1 - b0, gp.ctypes.data, int(n_thetas), int(nphis),
-                                            vec[0].ctypes.data, vec[1].ctypes.data, vec[2].ctypes.data,
-                                            tcs.ctypes.data, pcs.ctypes.data, ws.data_ptr(), ws.numel(),
-                                            stats[b0:b1].data_ptr(), stream))
-        raw = stats.cpu().numpy()
+        for dev, g0, g1, ws, stats, ev, st in work:
+            ev[0].record(st)
+        # batches issued round-robin over the devices: every launch is asynchronous, so they run concurrently
+        nb = max(-(-(g1 - g0) // groups_per_batch) for _, g0, g1, *_ in work)
+        for k in range(nb):
+            for dev, g0, g1, ws, stats, ev, st in work:
+                b0 = g0 + k * groups_per_batch
+                b1 = min(g1, b0 + groups_per_batch)
+                if b0 >= b1:
+                    continue
+                gp = np.ascontiguousarray(params[b0:b1])
+                C.check(C.lib().rtpb_spot_sweep(plan, dev.index or 0, b1 - b0, gp.ctypes.data, int(n_thetas),
+                                                int(nphis), vec[0].ctypes.data, vec[1].ctypes.data,
+                                                vec[2].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, ws.data_ptr(),
+                                                ws.numel(), stats[b0 - g0:b1 - g0].data_ptr(), st.cuda_stream))
+        for dev, g0, g1, ws, stats, ev, st in work:
+            ev[1].record(st)
+        raw = np.concatenate([stats[:g1 - g0].cpu().numpy() for _, g0, g1, _, stats, _, _ in work])
     dt = time.perf_counter() - t0
+    per_dev = []
+    for dev, g0, g1, ws, stats, ev, st in work:
+        ms = ev[0].elapsed_time(ev[1])
+        # HBM bytes of the fused sweep: the per-tile partial sums written and read back (the rays never
+        # leave the registers)
+        nbytes = (g1 - g0) * tiles * 7 * 8 * 2 + (g1 - g0) * 7 * 8
+        per_dev.append({"device": dev.index or 0, "groups": g1 - g0, "rays": (g1 - g0) * per, "kernel_ms": ms,
+                        "ray_surface_per_s": (g1 - g0) * per * S / (ms * 1e-3) if ms > 0 else None,
+                        "hbm_bytes": nbytes, "hbm_GBps": nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None})
     summ = summarize(raw.reshape(nf, nw, 7))
-    return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt}
+    return summ, {"seconds": dt, "rays": G * per, "ray_surface_per_s": G * per * S / dt, "per_device": per_dev}
 
 
 def _fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis, center_ray, code):

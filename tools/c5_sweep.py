@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--n-thetas", type=int, default=3163)
     ap.add_argument("--nphis", type=int, default=3162)
     ap.add_argument("--dtype", default="float64")
+    ap.add_argument("--devices", default="", help="in-process multi-GPU: 'all' or comma-separated GPU ids")
     args = ap.parse_args()
     import torch
     import ray_trace_pb_amd.materials as mat
@@ -44,8 +45,12 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    devices = None
+    if args.devices:
+        devices = list(range(torch.cuda.device_count())) if args.devices == "all" else \
+            [int(d) for d in args.devices.split(",")]
     summ, timing = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine, wls, theta, args.n_thetas,
-                                       args.nphis, device=dev, dtype=args.dtype)
+                                       args.nphis, device=dev, dtype=args.dtype, devices=devices)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -60,6 +65,7 @@ def main():
         print(json.dumps({"workload": "C5 spot sweep", "fields": len(fields), "wavelengths": len(wls),
                           "rays_per_group": args.n_thetas * args.nphis, "total_rays": rays, "surfaces": S,
                           "n_gpus": world, "seconds": wall, "ray_surface_per_s": rays * S / wall,
+                          "per_device_rank0": timing.get("per_device"),
                           "rank0_rms_radius_um_first_fields": (summ["rms_radius"][:2] * 1e3).tolist(),
                           "rank0_count_first_fields": summ["count"][:2].tolist()}))
     if world > 1:

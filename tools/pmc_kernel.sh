@@ -1,0 +1,28 @@
+#!/bin/bash
+# PMC passes over one command, summarised for the dispatches whose kernel name contains KERNEL
+# (one counter group per rocprofv3 run, --pmc only: no tracing domains).
+# usage: tools/pmc_kernel.sh OUTDIR KERNEL cmd...
+OUT=$1; KERNEL=$2; shift 2
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY" \
+           "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY" "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pmc -- "$@" > "$OUT/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i ($grp) rc=$rc"
+  if [ $rc -ge 124 ]; then exit $rc; fi
+done
+python3 - "$OUT" "$KERNEL" <<'PY'
+import csv, glob, os, sys, collections
+out, kern = sys.argv[1], sys.argv[2]
+agg = collections.defaultdict(list)
+for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for row in csv.DictReader(open(f)):
+        if kern in row["Kernel_Name"]:
+            agg[row["Counter_Name"]].append(float(row["Counter_Value"]))
+for k, v in sorted(agg.items()):
+    print(f"{k:28s} sum={sum(v):.6g} median={sorted(v)[len(v)//2]:.6g} n={len(v)}")
+PY
