@@ -104,7 +104,7 @@ template <typename T>
 __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     DevSurface<T> d;
     d.kind = p->kind;
-    d.pad = 0;
+    d.rcp_ok = p->rcp_ok;
     for (int j = 0; j < 3; ++j) {
         d.c[j] = p->c[j];
         d.nrm[j] = p->nrm[j];
@@ -112,6 +112,7 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     }
     d.R = p->R; d.R2 = p->R2; d.absR = p->absR; d.ap = p->ap; d.f = p->f; d.sin_a = p->sin_a; d.tol = p->tol;
     d.ap_sq = p->ap_sq; d.shell_lo = p->shell_lo; d.shell_hi = p->shell_hi;
+    d.rR = p->rR; d.rf = p->rf;
     return d;
 }
 

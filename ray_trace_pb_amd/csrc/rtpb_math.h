@@ -36,7 +36,7 @@ enum MatKind : int32_t { CONSTANT = 0, SELLMEIER = 1, POLY6 = 2, TABLE = 3,
 template <typename T>
 struct DevSurface {
     int32_t kind;
-    int32_t pad;
+    int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok)
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -52,6 +52,10 @@ struct DevSurface {
     T ap_sq;     // sqrt(s) <= ap           <=>  s <= ap_sq
     T shell_lo;  // |sqrt(s) - |R|| < tol   <=>  shell_lo <= s <= shell_hi
     T shell_hi;
+    // correctly rounded reciprocals of the surface's uniform divisors, computed on the host (the same y a
+    // per-lane make_rcp would refine, without its 5 VALU per lane per surface): 1 / radius, 1 / focal_len
+    T rR;
+    T rf;
 };
 
 template <typename T>
@@ -176,6 +180,20 @@ __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
     return __builtin_amdgcn_div_fixup(__builtin_fma(e, y, q0), b, a);
 }
 #endif
+
+// Rcp of a divisor whose reciprocal y = RN(1/b) the host computed: quotients through it are still correctly
+// rounded (Markstein: q0 = RN(a y) is within 1 ulp of a/b, r = fma(-b, q0, a) is exact, RN(q0 + r y) =
+// RN(a/b) when y = RN(1/b)); tests/test_gpu_fastdiv.py checks it on the same adversarial operands
+template <typename T>
+RTPB_HD Rcp<T> host_rcp(T b, T y, bool ok) {
+    return Rcp<T>{b, y, ok};
+}
+
+// host: the range test of fastdiv_den_ok
+inline bool host_rcp_ok(double b) {
+    const double m = std::fabs(b);
+    return (m >= 0x1p-120 && m <= 0x1p120) || b == 0.0 || std::isinf(b) || std::isnan(b);
+}
 
 template <typename T>
 RTPB_HD Rcp<T> make_rcp(T b) {
@@ -333,19 +351,28 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     return o;
 }
 
+// 0 < v < inf (v a positive normal or denormal number)
+template <typename T>
+RTPB_HD bool positive_finite(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, 0x180);    // +denormal | +normal
+#endif
+    return v > T(0) && v < T(1) / T(0);
+}
+
 // v / |v| with NaN components replaced by 0 (RT:1203-1209)
 template <typename T>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
     const T nrm = tsqrt<T>(x * x + y * y + z * z);
-#if defined(RTPB_EXP_RCP_NORMALIZE)      // experiment only: reciprocal multiply (NOT bit-exact)
-    const T inv = T(1) / nrm;
-    x = x * inv; y = y * inv; z = z * inv;
-#else
     div3(x, y, z, make_rcp(nrm));
-#endif
-    if (is_nan(x)) x = T(0);
-    if (is_nan(y)) y = T(0);
-    if (is_nan(z)) z = T(0);
+    // A NaN quotient needs a zero, infinite or NaN norm: when 0 < |v| < inf every component is finite and
+    // every quotient a number, so one class test skips the three per-component fix-ups (normal incidence,
+    // dead rows and garbage input take them)
+    if (__builtin_expect(!positive_finite(nrm), 0)) {
+        if (is_nan(x)) x = T(0);
+        if (is_nan(y)) y = T(0);
+        if (is_nan(z)) z = T(0);
+    }
 }
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
@@ -373,12 +400,12 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2) {
     o.dx = mag * cx + tang * Nx;
     o.dy = mag * cy + tang * Ny;
     o.dz = mag * cz + tang * Nz;
-    const bool bad = is_nan(o.dx);
-    o.x = bad ? qnan<T>() : ri.x;
-    o.y = bad ? qnan<T>() : ri.y;
-    o.z = bad ? qnan<T>() : ri.z;
+    o.x = ri.x; o.y = ri.y; o.z = ri.z;
     o.ph = ri.ph;
     o.wl = ri.wl;
+    if (__builtin_expect(is_nan(o.dx), 0)) {       // TIR (and dead rows): position NaN only (RT:1221)
+        o.x = qnan<T>(); o.y = qnan<T>(); o.z = qnan<T>();
+    }
     return o;
 }
 
@@ -393,12 +420,12 @@ RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz) {
     o.dx = mag_na * Nx + mag_nc * cx;
     o.dy = mag_na * Ny + mag_nc * cy;
     o.dz = mag_na * Nz + mag_nc * cz;
-    const bool bad = is_nan(o.dx);
-    o.x = bad ? qnan<T>() : ri.x;
-    o.y = bad ? qnan<T>() : ri.y;
-    o.z = bad ? qnan<T>() : ri.z;
+    o.x = ri.x; o.y = ri.y; o.z = ri.z;
     o.ph = ri.ph;
     o.wl = ri.wl;
+    if (__builtin_expect(is_nan(o.dx), 0)) {       // position NaN where the direction is (RT:1289)
+        o.x = qnan<T>(); o.y = qnan<T>(); o.z = qnan<T>();
+    }
     return o;
 }
 
@@ -457,7 +484,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         o.x = n1 * f * sin_t1 * spx + Bx;
         o.y = n1 * f * sin_t1 * spy + By;
         o.z = n1 * f * sin_t1 * spz + Bz;
-        const T sin_t2 = -r1n / f / n2;
+        const T sin_t2 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0)) / n2;
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2);
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
@@ -476,7 +503,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             Nx = ri.x - s.c[0];                                            // (p - c) / R, RT:1476
             Ny = ri.y - s.c[1];
             Nz = ri.z - s.c[2];
-            div3(Nx, Ny, Nz, make_rcp(s.R));
+            div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0));
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
             ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl);   // RT:1331-1337, 1398-1403
@@ -604,6 +631,9 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     d.tol = s.on_tol;
     d.ap_sq = host::sqrt_le_bound(s.aperture);
     host::shell_bounds(d.absR, s.on_tol, d.shell_lo, d.shell_hi);
+    d.rR = 1.0 / s.radius;                       // IEEE division: RN(1/R) (inf for R = 0)
+    d.rf = 1.0 / s.focal_len;
+    d.rcp_ok = (host_rcp_ok(s.radius) ? 1 : 0) | (host_rcp_ok(s.focal_len) ? 2 : 0);
     return d;
 }
 

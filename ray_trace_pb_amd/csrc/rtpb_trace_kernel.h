@@ -228,17 +228,22 @@ hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
         if (w == 5) return launch_w<TI, T, IL, OL, ST, 5, 15>(a, st);
     }
 #if defined(RTPB_EXP_WPE)                  // experiment only: minimum waves per SIMD for every variant
-    constexpr int kW = RTPB_EXP_WPE;
+#define RTPB_WPE(F) RTPB_EXP_WPE
 #else
-    constexpr int kW = 1;
+    // float64 final-plane-only kernels (compute-bound: the C5 / focus-finding mode) are held to >= 6
+    // waves per SIMD (<= 80 VGPRs, no spill); everything else keeps the compiler's choice (the history
+    // kernels are bound by their LDS tiles and store stream: 6-8 waves measured no faster; the float32
+    // final-only variants would spill)
+#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? 6 : 1)
 #endif
     switch (feat) {
-    case 0: return launch_w<TI, T, IL, OL, ST, kW, 0>(a, st);
-    case 1: return launch_w<TI, T, IL, OL, ST, kW, 1>(a, st);
-    case 4: return launch_w<TI, T, IL, OL, ST, kW, 4>(a, st);
-    case 5: return launch_w<TI, T, IL, OL, ST, kW, 5>(a, st);
-    default: return launch_w<TI, T, IL, OL, ST, kW, 15>(a, st);    // POLY6 or a large table: everything in
+    case 0: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(0), 0>(a, st);
+    case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
+    case 4: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(4), 4>(a, st);
+    case 5: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(5), 5>(a, st);
+    default: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(15), 15>(a, st);   // POLY6 or a large table: everything in
     }
+#undef RTPB_WPE
 }
 
 template <typename TI, typename T>

@@ -14,9 +14,10 @@ using namespace rtpb;
 namespace {
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
-//      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a)
+//      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
+//      [8] div1(a, host_rcp(b, yh)) with yh = the host's RN(1 / b) (the descriptors' rR / rf)
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
-                             const unsigned char* kill, int64_t n, double* out) {
+                             const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double ai = a[i], bi = b[i];
@@ -32,30 +33,34 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[5 * n + i] = div1_as(ai, bb, r);
     out[6 * n + i] = tsqrt<double>(bi);
     out[7 * n + i] = tsqrt<double>(ai);
+    const double mb = fabs(bi);          // host_rcp_ok (rtpb_math.h), the flag lower_surface stores
+    const bool ok = (mb >= 0x1p-120 && mb <= 0x1p120) || bi == 0.0 || isinf(bi) || isnan(bi);
+    out[8 * n + i] = div1(ai, host_rcp(bi, yh[i], ok));
 }
 
 }  // namespace
 
 extern "C" int fastdiv_check(const double* a, const double* a2, const double* a3, const double* b,
-                             const unsigned char* kill, int64_t n, double* out) {
+                             const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const size_t bytes = static_cast<size_t>(n) * sizeof(double);
-    const double* src[4] = {a, a2, a3, b};
-    double* dev[4] = {nullptr, nullptr, nullptr, nullptr};
+    const double* src[5] = {a, a2, a3, b, yh};
+    double* dev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     double* dout = nullptr;
     unsigned char* dk = nullptr;
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
+    for (int k = 0; k < 5 && e == hipSuccess; ++k) {
         e = hipMalloc(&dev[k], bytes);
         if (e == hipSuccess) e = hipMemcpy(dev[k], src[k], bytes, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipMalloc(&dk, static_cast<size_t>(n));
     if (e == hipSuccess) e = hipMemcpy(dk, kill, static_cast<size_t>(n), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&dout, 8 * bytes);
+    if (e == hipSuccess) e = hipMalloc(&dout, 9 * bytes);
     if (e == hipSuccess) {
-        check_kernel<<<static_cast<unsigned>((n + 255) / 256), 256>>>(dev[0], dev[1], dev[2], dev[3], dk, n, dout);
+        check_kernel<<<static_cast<unsigned>((n + 255) / 256), 256>>>(dev[0], dev[1], dev[2], dev[3], dev[4], dk, n,
+                                                                      dout);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(out, dout, 8 * bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, 9 * bytes, hipMemcpyDeviceToHost);
     for (double* p : dev) (void)hipFree(p);
     (void)hipFree(dk);
     (void)hipFree(dout);

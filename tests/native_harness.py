@@ -67,17 +67,20 @@ def build_fastdiv():
 
 
 def fastdiv_check(a, a2, a3, b, kill):
-    """(8, n) float64: div1, a / b, div3 x/y/z, div1_as, tsqrt(b), tsqrt(a) -- computed on cuda:0."""
+    """(9, n) float64: div1, a / b, div3 x/y/z, div1_as, tsqrt(b), tsqrt(a), div1 through the host's
+    reciprocal RN(1/b) -- computed on cuda:0."""
     global _fastdiv
     if _fastdiv is None:
         import torch  # noqa: F401 -- one HIP runtime per process: bind to torch's
         _fastdiv = ctypes.CDLL(build_fastdiv())
-        _fastdiv.fastdiv_check.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
+        _fastdiv.fastdiv_check.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_int64, ctypes.c_void_p]
         _fastdiv.fastdiv_check.restype = ctypes.c_int
-    arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, a2, a3, b)]
+    with np.errstate(all="ignore"):
+        yh = 1.0 / np.asarray(b, dtype=np.float64)
+    arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, a2, a3, b, yh)]
     k = np.ascontiguousarray(kill, dtype=np.uint8)
     n = arrs[0].size
-    out = np.empty((8, n), dtype=np.float64)
+    out = np.empty((9, n), dtype=np.float64)
     rc = _fastdiv.fastdiv_check(*[x.ctypes.data for x in arrs], k.ctypes.data, n, out.ctypes.data)
     assert rc == 0, rc
     return out

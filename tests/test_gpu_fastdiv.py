@@ -32,6 +32,7 @@ def _check(a, a2, a3, b, kill):
         _same(out[5], a / bb)            # div1_as
         _same(out[6], np.sqrt(b))        # tsqrt
         _same(out[7], np.sqrt(a))
+        _same(out[8], a / b)             # div1 with the host's reciprocal (descriptor rR / rf)
 
 
 def _rand_bits(rng, n):
