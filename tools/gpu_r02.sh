@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-2 GPU session on one MI355X: parity tests, smoke, the C3 headline bench (+C2 secondary, PMC
-# traffic, CPU baseline) and the rocprofv3 kernel-trace summary of the same bench command.  Every GPU step
-# has its own time limit; a crash/abort/timeout stops the script, test failures (exit 1) do not.
+# traffic, CPU baseline), the rocprofv3 kernel-trace summary of the same bench command, PMC passes of the
+# C3 trace kernel, a 2-rank torchrun rehearsal sharing the GPU, and the C3/C4 full-size configs.  Every GPU
+# step has its own time limit; a crash/abort/timeout stops the script, test failures (exit 1) do not.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r02}
@@ -23,4 +24,9 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 step bench 900 python bench.py
 step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof -o bench -- python3 bench.py --cpu-baseline off --traffic off
+if [ -z "$SKIP_EXTRA" ]; then
+  step pmc_c3 900 bash tools/pmc_kernel.sh $P/pmc_c3 trace_kernel python3 bench.py --pmc-child --config c3
+  step bench_2ranks_1gpu 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 3
+  step configs_c3_c4_full 900 python tools/configs_full.py
+fi
 exit 0
