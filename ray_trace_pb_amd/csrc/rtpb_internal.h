@@ -143,6 +143,18 @@ __device__ __forceinline__ Ray<double> load_ray(const TS* __restrict__ in, int64
     } else {
         r.x = in[i]; r.y = in[fs + i]; r.z = in[2 * fs + i]; r.dx = in[3 * fs + i];
         r.dy = in[4 * fs + i]; r.dz = in[5 * fs + i]; r.ph = in[6 * fs + i]; r.wl = in[7 * fs + i];
+#if defined(__HIP_DEVICE_COMPILE__)
+        // Codegen workaround (ROCm 7.2 LLVM, float64 SoA-input kernels): with the eight fields defined by
+        // separate 64-bit loads, the greedy allocator splits the (ph, wl) 128-bit tuple that feeds the
+        // ds_write_b128 of the staged record and the rewriter marks the split copy's source undef, so the
+        // phase after the first surface was lost (-0.0).  Defining the four pairs as whole 128-bit values,
+        // as the AoS loads do, avoids it.  tests/test_codegen_guard.py scans every kernel's assembly for
+        // the signature (a 64-bit KILL of another register pair).
+        typedef double v2d __attribute__((ext_vector_type(2)));
+        v2d a = {r.x, r.y}, b = {r.z, r.dx}, c = {r.dy, r.dz}, d = {r.ph, r.wl};
+        asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+        r.x = a.x; r.y = a.y; r.z = b.x; r.dx = b.y; r.dy = c.x; r.dz = c.y; r.ph = d.x; r.wl = d.y;
+#endif
     }
     return r;
 }

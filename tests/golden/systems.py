@@ -414,6 +414,92 @@ def lightsheet(rt, mat, rad_curv, nrays=1001):
     return osys, rays, mat.Vacuum(), mat.Vacuum()
 
 
+# ------------------------------------------------------------------ randomised systems (fuzz)
+FUZZ_GLASSES = ("Bk7", "Sf10", "Sf2", "Nsf11", "Nbaf10", "FusedSilica", "Nlak22", "Nsf6ht", "Nsk11")
+N_FUZZ = 16
+
+
+def _tilted(rng, axis, p, scale):
+    axis = np.asarray(axis, dtype=float)
+    if rng.random() >= p:
+        return axis
+    return unit(axis + np.array([1.0, 1.0, 0.0]) * rng.normal(scale=scale, size=3))
+
+
+def fuzz(rt, mat, seed, nrays=160):
+    """A seeded random system and bundle: 2-9 surfaces drawn from every kind (flats, spheres of either
+    sign from R=4 to 2000 plus the occasional R=1e6, perfect lenses, plane mirrors that turn the
+    bundle round), tilted and decentred at random, any medium between them (Vacuum, Constant,
+    Sellmeier glasses, the Ebaf11 polynomial, a user n()), and a bundle that is a point-source fan,
+    a tilted collimated beam or random rays -- with a few non-unit directions and the hand-placed
+    oddities of ``stress_rays``.  The golden files hold the reference's answer for each seed."""
+    rng = np.random.default_rng(SEED + 1000 + seed)
+    Cauchy = cauchy_class(mat)
+
+    def medium():
+        u = rng.random()
+        if u < 0.35:
+            return mat.Vacuum()
+        if u < 0.5:
+            return mat.Constant(float(np.round(rng.uniform(1.0, 1.9), 4)))
+        if u < 0.58:
+            return mat.Ebaf11()
+        if u < 0.64:
+            return Cauchy(a=float(np.round(rng.uniform(1.4, 1.7), 4)), b=float(np.round(rng.uniform(0.002, 0.01), 5)))
+        return getattr(mat, FUZZ_GLASSES[rng.integers(len(FUZZ_GLASSES))])()
+
+    S = int(rng.integers(2, 10))
+    sgn, z = 1.0, 0.0
+    surfaces, materials = [], []
+    for k in range(S):
+        u = rng.random()
+        ap = float(np.round(rng.uniform(3, 30), 3))
+        shift = np.array([1.0, 1.0, 0.0]) * rng.normal(scale=1.0, size=3) if rng.random() < 0.3 else np.zeros(3)
+        c = np.array([0.0, 0.0, z]) + shift
+        if u < 0.3:
+            surfaces.append(rt.FlatSurface(c, _tilted(rng, [0, 0, sgn], 0.3, 0.08), ap))
+        elif u < 0.72:
+            axis = _tilted(rng, [0, 0, sgn], 0.25, 0.05)
+            R = float(rng.choice([-1.0, 1.0]) * np.round(np.exp(rng.uniform(np.log(4), np.log(2000))), 3))
+            if rng.random() < 0.06:
+                R = float(np.sign(R) * 1e6)
+            surfaces.append(rt.SphericalSurface(R, c + R * axis, ap, input_axis=axis))
+        elif u < 0.9:
+            f = float(np.round(rng.uniform(5, 60), 3))
+            surfaces.append(rt.PerfectLens(f, c, _tilted(rng, [0, 0, sgn], 0.2, 0.03),
+                                           float(np.round(rng.uniform(0.2, 1.3), 3))))
+        else:
+            surfaces.append(rt.PlaneMirror(c, _tilted(rng, [0, 0, -sgn], 0.5, 0.05), 2 * ap))
+            sgn = -sgn
+        if k < S - 1:
+            materials.append(medium())
+        z += sgn * float(np.round(rng.uniform(3, 25), 3))
+
+    mode = int(rng.integers(3))
+    wl = float(rng.choice([0.405, 0.488, 0.532, 0.6328, 0.785, 1.0]))
+    src = np.array([rng.normal(scale=0.5), rng.normal(scale=0.5), -float(rng.uniform(2, 20))])
+    if mode == 0:
+        center = np.array([0.0, 0.0, 1.0])
+        for _ in range(8):                   # get_ray_fan demands norm(center_ray) == 1 exactly (RT:67-68)
+            c = _tilted(rng, [0, 0, 1], 0.7, 0.05)
+            if np.linalg.norm(c) == 1:
+                center = c
+                break
+        rays = rt.get_ray_fan(src, float(rng.uniform(0.05, 0.6)), 20, wl, nphis=8, center_ray=tuple(center))
+    elif mode == 1:
+        rays = rt.get_collimated_rays(src, float(rng.uniform(1, 20)), 20, wl, nphis=8,
+                                      normal=_tilted(rng, [0, 0, 1], 0.7, 0.05))
+    else:
+        rays = stress_rays(nrays, seed=SEED + 2000 + seed)
+        rays[8:, 2] += src[2] + 10
+    rays = np.array(rays[:nrays], dtype=np.float64)
+    if mode != 2:
+        rays[:, 6] = rng.uniform(0, 10, rays.shape[0])
+        odd = rng.random(rays.shape[0]) < 0.05                  # non-unit directions
+        rays[odd, 3:6] *= rng.uniform(0.5, 2.0, (int(odd.sum()), 1))
+    return rt.System(surfaces, materials), rays, medium(), medium()
+
+
 # name -> recipe; every recipe returns (system, rays, initial_material, final_material)
 RECIPES = {
     "c1_plano_convex": c1_plano_convex,
@@ -433,10 +519,12 @@ RECIPES = {
     "lightsheet_r120": lambda rt, mat: lightsheet(rt, mat, 120.0),
     "lightsheet_r1e9": lambda rt, mat: lightsheet(rt, mat, 1e9),
 }
+RECIPES.update({"fuzz_%02d" % k: (lambda rt, mat, k=k: fuzz(rt, mat, k)) for k in range(N_FUZZ)})
 
 # recipes also recorded with their input rays rounded to float32 (<name>_f32in.npz): the reference's
 # answer for float32 input, which the float32-input paths must reproduce
-F32_INPUT_CASES = ("c2_achromat", "c3_relay", "c4_opm", "c5_odt", "stress")
+F32_INPUT_CASES = ("c2_achromat", "c3_relay", "c4_opm", "c5_odt", "stress", "fuzz_00", "fuzz_06", "fuzz_11",
+                   "fuzz_14")
 
 
 # ------------------------------------------------------------------ long systems (> RTPB_MAX_SURFACES)

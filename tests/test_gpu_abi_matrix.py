@@ -1,0 +1,129 @@
+"""Every kernel variant behind rtpb_trace (include/rtpb.h:139-142), called through the C ABI on padded,
+strided device buffers, for every golden case (the reference's own histories, incl. the randomised
+fuzz_* systems): storage type x input type x input layout x output layout x plane selection.
+
+  * float64 rays -> float64 storage: the reference history, bit for bit;
+  * float64 rays -> float32 storage: the reference history rounded once;
+  * float32 rays: the oracle's float64 trace of the exactly widened input (rounded once for float32
+    storage);
+  * SoA input (plan dtype only) and SoA output with field strides larger than the bundle, AoS output
+    with a plane stride larger than 8 N: the padding between slots/fields must stay untouched.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from ray_trace_pb_amd import _capi as C  # noqa: E402
+from ray_trace_pb_amd import _engine as E  # noqa: E402
+from oracle import rt_numpy as O  # noqa: E402
+from parity import CASES, GOLDEN  # noqa: E402
+from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+PAD = 13                    # extra rays of padding per SoA field / AoS slot
+SENTINEL = 12345.0
+TORCH_DT = {C.RTPB_F64: torch.float64, C.RTPB_F32: torch.float32}
+NP_DT = {C.RTPB_F64: np.float64, C.RTPB_F32: np.float32}
+
+
+def _load(name):
+    d = np.load(f"{GOLDEN}/{name}.npz")
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    return system, [m0] + list(system.materials) + [m1], d["rays_in"], d["history"]
+
+
+def _selections(P, rng):
+    sub = sorted(set([0, P - 1] + list(rng.choice(P, size=min(P, 4), replace=False))))
+    return {"all": list(range(P)), "final": [P - 1], "subset": [int(p) for p in sub]}
+
+
+def _device_input(rays, in_code, in_layout):
+    n = rays.shape[0]
+    x = torch.from_numpy(np.ascontiguousarray(rays.astype(NP_DT[in_code]))).to(DEV)
+    if in_layout == C.RTPB_AOS:
+        return x, x, 0
+    buf = torch.full((8, n + PAD), SENTINEL, dtype=TORCH_DT[in_code], device=DEV)
+    buf[:, :n] = x.t()
+    return buf, x, n + PAD
+
+
+def _trace(plan, x, in_code, in_layout, in_stride, n, nslots, out_code, out_layout):
+    """Output buffer filled with SENTINEL; returns (slots as (nslots, n, 8) numpy, padding untouched?)."""
+    if out_layout == C.RTPB_AOS:
+        plane_stride, field_stride = 8 * (n + PAD), 0
+    else:
+        field_stride = n + PAD
+        plane_stride = 8 * field_stride + 5
+    out = torch.full((max(nslots, 1) * plane_stride,), SENTINEL, dtype=TORCH_DT[out_code], device=DEV)
+    lo_hi = plan[1]
+    C.check(C.lib().rtpb_trace(plan[0], 0, x.data_ptr(), in_code, n, in_layout, in_stride, out.data_ptr(), out_layout,
+                               plane_stride, field_stride, lo_hi[0], lo_hi[1],
+                               torch.cuda.current_stream(DEV).cuda_stream))
+    torch.cuda.synchronize(DEV)
+    flat = out.cpu().numpy()
+    slots, mask = [], np.ones(flat.shape, dtype=bool)
+    for s in range(nslots):
+        base = s * plane_stride
+        if out_layout == C.RTPB_AOS:
+            slots.append(flat[base:base + 8 * n].reshape(n, 8))
+            mask[base:base + 8 * n] = False
+        else:
+            f = np.stack([flat[base + k * field_stride: base + k * field_stride + n] for k in range(8)], axis=1)
+            slots.append(f)
+            for k in range(8):
+                mask[base + k * field_stride: base + k * field_stride + n] = False
+    pad_ok = bool(np.all(flat[mask] == SENTINEL))
+    return np.stack(slots) if slots else np.zeros((0, n, 8), NP_DT[out_code]), pad_ok
+
+
+KNOBS = [None, ("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1), ("waves_per_eu", 5)]
+KNOB_DEFAULT = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0}
+
+
+@pytest.fixture(params=KNOBS, ids=lambda k: "default" if k is None else "%s=%d" % k)
+def knob(request):
+    """Every store/load strategy of the tuning knobs (include/rtpb.h rtpb_set_tuning) selects other kernel
+    instantiations; all of them must give the same histories."""
+    k = request.param
+    if k is not None:
+        C.check(C.lib().rtpb_set_tuning(k[0].encode(), k[1]))
+    yield k
+    if k is not None:
+        C.check(C.lib().rtpb_set_tuning(k[0].encode(), KNOB_DEFAULT[k[0]]))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_c_abi_variant_matrix(name, knob):
+    system, materials, rays, ref = _load(name)
+    n, S = rays.shape[0], len(system.surfaces)
+    if S > C.RTPB_MAX_SURFACES:
+        pytest.skip("segmented systems go through raytrace.trace_surfaces")
+    P = 2 * S + 1
+    widened = rays.astype(np.float32).astype(np.float64)
+    ref32in = O.ray_trace([surface_to_dict(s) for s in system.surfaces], [material_to_dict(m) for m in materials],
+                          widened)
+    sels = _selections(P, np.random.default_rng(n + S))
+    checked = 0
+    for in_code in (C.RTPB_F64, C.RTPB_F32):
+        traced = rays if in_code == C.RTPB_F64 else widened       # the table keys are the traced wavelengths
+        for out_code in (C.RTPB_F64, C.RTPB_F32):
+            expect = (ref if in_code == C.RTPB_F64 else ref32in).astype(NP_DT[out_code])
+            low = E.lower(system.surfaces, materials, lambda: E.distinct_wavelengths(traced[:, 7]), out_code)
+            with E.plan_ref(low) as plan:
+                for in_layout in (C.RTPB_AOS, C.RTPB_SOA):
+                    if in_layout == C.RTPB_SOA and in_code != out_code:
+                        continue
+                    x, _, in_stride = _device_input(rays, in_code, in_layout)
+                    for out_layout in (C.RTPB_AOS, C.RTPB_SOA):
+                        for sname, sel in sels.items():
+                            got, pad_ok = _trace((plan, E.plane_mask(sel)), x, in_code, in_layout, in_stride, n,
+                                                 len(sel), out_code, out_layout)
+                            key = (out_code, in_code, in_layout, out_layout, sname)
+                            assert pad_ok, key
+                            assert np.array_equal(got, expect[sel], equal_nan=True), key
+                            checked += 1
+    assert checked == 2 * 3 * 2 * 3
