@@ -433,7 +433,8 @@ def _hooked(system, spheres=True):
     return rt.System(out, system.materials)
 
 
-@pytest.mark.parametrize("name", ["stress", "c4_mirror", "c2_achromat", "tir_prism", "c1_plano_convex"])
+@pytest.mark.parametrize("name", ["stress", "c4_mirror", "c2_achromat", "tir_prism", "c1_plano_convex"] +
+                         [c for c in CASES if c.startswith("fuzz_")])
 def test_user_geometry_hooks_bitwise_vs_reference(name):
     """User geometry hooks + GPU front-side / Snell / reflection reproduce the reference history
     exactly, including misses, back-facing rays, TIR, aperture clipping and user materials."""
