@@ -233,32 +233,44 @@ __device__ __forceinline__ void tile_write(uint4* __restrict__ tile, int lane, c
     }
 }
 
+// A wave-uniform 64-bit value the divergence analysis cannot prove uniform (e.g. derived from threadIdx.x
+// & ~63): moved to SGPRs so the address arithmetic that uses it is scalar.
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32))) << 32) |
+           static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v)));
+}
+
 // Write the wave's staged block (64 records) to `plane` lane-contiguously: 1 KiB per store instruction.
 // Callers wait for the tile writes first (lgkmcnt(0)); the compiler waits for the tile reads before the
 // global stores that consume them, and a wave's DS operations execute in order, so the next tile_write
 // cannot overtake these reads.
+// The stores are raw buffer stores through a per-wave resource (SGPRs): base = the block's first record,
+// num_records = the block's bytes, so the address is lane*16 + an immediate and the bounds check of the
+// buffer unit drops the tail of the last block -- no 64-bit VALU address arithmetic and no exec-mask
+// branches per plane.  (ray0 and the plane pointer are wave-uniform; readfirstlane tells the compiler.)
 template <typename TS, bool NT>
 __device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
                                            int64_t n, int lane) {
+    constexpr int kRec = 8 * sizeof(TS);
+    constexpr int kAux = NT ? 2 : 0;                     // gfx950 cache policy: nt
+    const int64_t left = n - ray0;
+    const int nbytes = static_cast<int>((left < 64 ? left : 64) * kRec);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(uniform_u64(reinterpret_cast<uint64_t>(plane + ray0 * 8))), static_cast<short>(0),
+        __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u* t = reinterpret_cast<const v4u*>(tile);
     if constexpr (sizeof(TS) == 8) {
-        const double2* t = reinterpret_cast<const double2*>(tile);
-        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 4;
-        double2* g = reinterpret_cast<double2*>(plane + ray0 * 8);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = lane + 64 * j, rr = c >> 2, pp = c & 3;
-            const double2 v = t[4 * rr + (pp ^ ((rr >> 1) & 3))];
-            if (c < nchunks) gstore(g + c, v, NT);
+            __builtin_amdgcn_raw_buffer_store_b128(t[4 * rr + (pp ^ ((rr >> 1) & 3))], rsrc, c * 16, 0, kAux);
         }
     } else {
-        const float4* t = reinterpret_cast<const float4*>(tile);
-        const int64_t nchunks = (n - ray0 < 64 ? n - ray0 : 64) * 2;
-        float4* g = reinterpret_cast<float4*>(plane + ray0 * 8);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int c = lane + 64 * j, rr = c >> 1, pp = c & 1;
-            const float4 v = t[2 * rr + (pp ^ ((rr >> 2) & 1))];
-            if (c < nchunks) gstore(g + c, v, NT);
+            __builtin_amdgcn_raw_buffer_store_b128(t[2 * rr + (pp ^ ((rr >> 2) & 1))], rsrc, c * 16, 0, kAux);
         }
     }
 }

@@ -87,7 +87,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
 #else
     const int64_t i = blk * kB + threadIdx.x;
 #endif
-    const int64_t ray0 = i - lane;                       // first ray of this wave
+    const int64_t ray0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(i - lane)));  // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
 #if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
     // consecutive workgroups go to different XCDs, so the delay step uses blockIdx / 8 (varies inside
