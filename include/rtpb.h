@@ -255,6 +255,18 @@ int rtpb_grid_interpolate(int32_t device, const rtpb_triangulation* tri, const d
                           const double* ys, int64_t ny, double radius, double* phase_out, double* field_out,
                           void* stream);
 
+/* ---- distinct wavelengths of a device-resident bundle (keys of the plan's RTPB_TABLE materials) -- */
+/* Replaces the host-side np.unique of the wavelength column that tabulated materials need
+   (MAT:128-144 Ebaf11 and user Material.n are evaluated by the host at exactly these wavelengths).
+   col: device pointer to the first wavelength, `stride` elements between consecutive rays (8 for an
+   (N, 8) AoS bundle), n values of `dtype` (RTPB_F64 / RTPB_F32, widened exactly).  table: device buffer
+   of `table_slots` uint64 (a power of two); max_keys <= table_slots / 2; count: one device uint32.
+   Asynchronous on `stream`.  Afterwards the table holds the distinct keys as float64 bit patterns (all
+   NaNs as one quiet-NaN key, -0.0 as +0.0) in arbitrary order, empty slots = all-ones; *count is the
+   number of keys, or > max_keys when there are more (the caller then sorts instead). */
+int rtpb_distinct_keys(int32_t device, const void* col, int32_t dtype, int64_t n, int64_t stride, uint64_t* table,
+                       int32_t table_slots, int32_t max_keys, uint32_t* count, void* stream);
+
 /* ---- tuning knobs (benchmarks / A-B tests; process-wide) ------------------------------------ */
 /* "aos_staging": 1 (default) = AOS planes are written through a per-wave LDS tile so every global
    store instruction writes 1 KiB contiguous; 0 = direct 16-byte stores at the record stride.

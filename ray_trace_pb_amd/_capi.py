@@ -70,6 +70,7 @@ SIGNATURES = {
     "rtpb_spot_sweep": (ctypes.c_int, [_P, _i32, _i64, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _i64, _P, _P]),
     "rtpb_grid_interpolate": (ctypes.c_int, [_i32, ctypes.POINTER(Triangulation), _P, _i64, _P, _i64,
                                              ctypes.c_double, _P, _P, _P]),
+    "rtpb_distinct_keys": (ctypes.c_int, [_i32, _P, _i32, _i64, _i64, _P, _i32, _i32, _P, _P]),
     "rtpb_front_side": (ctypes.c_int, [_P, _i32, _P, _P, _i64, _P, _P]),
     "rtpb_interact": (ctypes.c_int, [_P, _i32, _i32, _P, _P, _P, _i64, _P, _P]),
     "rtpb_spot_stats": (ctypes.c_int, [_i32, _i32, _P, _i64, _i64, _P, _i64, _P, _P]),

@@ -90,11 +90,39 @@ def lower(surfaces, materials, wavelengths, dtype):
     return low
 
 
+DISTINCT_SLOTS = 8192
+DISTINCT_MAX_KEYS = 4096
+
+
+def _distinct_device(col):
+    """Distinct wavelengths of a torch CUDA column with rtpb_distinct_keys (one pass, hash set in HBM);
+    None when there are more than DISTINCT_MAX_KEYS of them."""
+    import torch
+    if col.dtype not in (torch.float64, torch.float32):
+        col = col.double()
+    ws = torch.empty(DISTINCT_SLOTS + 1, dtype=torch.int64, device=col.device)
+    lib = C.lib()
+    C.check(lib.rtpb_distinct_keys(col.device.index, col.data_ptr(),
+                                   C.RTPB_F32 if col.dtype == torch.float32 else C.RTPB_F64, col.shape[0],
+                                   max(col.stride(0), 1), ws.data_ptr(), DISTINCT_SLOTS, DISTINCT_MAX_KEYS,
+                                   ws.data_ptr() + 8 * DISTINCT_SLOTS, torch.cuda.current_stream(col.device).cuda_stream))
+    host = ws.cpu().numpy()
+    if int(host[-1] & 0xFFFFFFFF) > DISTINCT_MAX_KEYS:
+        return None
+    keys = host[:DISTINCT_SLOTS].view(np.uint64)
+    return np.unique(keys[keys != np.uint64(0xFFFFFFFFFFFFFFFF)].view(np.float64))
+
+
 def distinct_wavelengths(col):
     """Sorted distinct values of a wavelength column (NumPy or torch CUDA), NaN last -- the keys of
-    RTPB_TABLE materials.  Single-colour bundles (the common case) skip the sort."""
+    RTPB_TABLE materials.  Single-colour NumPy bundles (the common case) skip the sort; torch CUDA
+    columns go through the rtpb_distinct_keys pass (a sort only beyond DISTINCT_MAX_KEYS colours)."""
     if type(col).__module__.startswith("torch"):
         import torch
+        if col.is_cuda and col.dim() == 1:
+            keys = _distinct_device(col)
+            if keys is not None:
+                return keys
         return np.unique(torch.unique(col.double()).cpu().numpy())
     w = np.asarray(col, dtype=np.float64)
     if w.size and (w == w[0]).all():
