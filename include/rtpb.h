@@ -276,7 +276,11 @@ int rtpb_distinct_keys(int32_t device, const void* col, int32_t dtype, int64_t n
    0 (default) = 4 x 16-byte loads per lane.
    "waves_per_eu": 0 (default: compiler choice, 4 waves/SIMD) or 5 = occupancy target for the
    AOS->AOS staged kernel (the compiler then spills to scratch to fit).
-   "host_chunk_mib": input + output bytes per pipelined chunk of rtpb_trace_host (default 128). */
+   "host_chunk_mib": input + output bytes per pipelined chunk of rtpb_trace_host (default 128).
+   "indexed_materials": 1 (default) = plans created from now on whose TABLE materials all share one
+   key set (and that have no POLY6 material) also tabulate every other material at those keys, so the
+   kernel reads n from LDS instead of evaluating Sellmeier dispersion per surface (bit-identical: the
+   host evaluates the kernel's own material_n); 0 = evaluate per surface. */
 int rtpb_set_tuning(const char* key, int64_t value);
 
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */

@@ -201,6 +201,17 @@ def plan_ref(low):
         _release(p)
 
 
+def clear_plan_cache():
+    """Drop every cached plan (plans in use are freed by their last user).  Plans read some knobs at
+    creation (rtpb_set_tuning "indexed_materials"), so tests toggling them start from an empty cache."""
+    with _plans_lock:
+        while _PLANS:
+            _, old = _PLANS.popitem(last=False)
+            old.evicted = True
+            if old.users == 0:
+                old.lib.rtpb_plan_destroy(old.ptr)
+
+
 def plan_for(low):
     """The cached plan's raw pointer (single-threaded tools; library paths use plan_ref)."""
     p = _acquire(low)

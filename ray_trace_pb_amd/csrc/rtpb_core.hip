@@ -25,7 +25,67 @@ template <typename T>
 void blob_layout(rtpb_plan& p) {
     p.off_mats = align256(p.surf.size() * sizeof(DevSurface<T>));
     p.off_table = p.off_mats + align256(p.mats.size() * sizeof(DevMaterial<T>));
-    p.blob_bytes = p.off_table + align256(std::max<size_t>(p.table.size(), 2) * sizeof(T));
+    p.off_itab = p.off_table + align256(std::max<size_t>(p.table.size(), 2) * sizeof(T));
+    p.blob_bytes = p.off_itab + align256(std::max<size_t>(p.itab.size(), 2) * sizeof(T));
+}
+
+// The device material descriptor of plan material k (zero-coefficient Sellmeier = VACUUM, as the
+// kernels see it).
+DevMaterial<double> device_material(const rtpb_plan& p, size_t k) {
+    const rtpb_material& m = p.mats[k];
+    DevMaterial<double> d{};
+    d.kind = m.kind;
+    bool zero = m.kind == RTPB_SELLMEIER;
+    for (int j = 0; j < 6; ++j) {
+        d.c[j] = m.c[j];
+        zero = zero && m.c[j] == 0.0;
+    }
+    if (zero) d.kind = VACUUM;
+    d.table_off = p.table_off[k];
+    d.table_len = m.kind == RTPB_TABLE ? m.table_len : 0;
+    return d;
+}
+
+// Indexed materials (kLdsIndexedDoubles): when every TABLE material shares one strictly increasing key
+// set (NaN last allowed) and there is no POLY6 material, tabulate every material at those keys --
+// TABLE materials by their own values, the others with material_n itself (host build of the kernel's
+// function, -ffp-contract=off: the same IEEE operations, hence the same bits).
+void build_indexed(rtpb_plan& p) {
+    if (p.table.empty() || (p.feat & 2)) return;
+    const size_t M = p.mats.size();
+    int first = -1;
+    for (size_t k = 0; k < M; ++k)
+        if (p.mats[k].kind == RTPB_TABLE) { first = static_cast<int>(k); break; }
+    if (first < 0) return;
+    const int K = p.mats[first].table_len;
+    if (K <= 0 || static_cast<size_t>(K) * (M + 1) > static_cast<size_t>(kLdsIndexedDoubles)) return;
+    const double* keys0 = p.table.data() + 2 * static_cast<size_t>(p.table_off[first]);
+    for (int j = 0; j < K; ++j) {
+        const double kj = keys0[2 * j];
+        if (kj != kj && j != K - 1) return;                               // NaN only as the last key
+        if (j > 0 && kj == kj && !(keys0[2 * (j - 1)] < kj)) return;       // strictly increasing
+    }
+    for (size_t k = 0; k < M; ++k) {                                      // one key set for every table
+        if (p.mats[k].kind != RTPB_TABLE) continue;
+        if (p.mats[k].table_len != K) return;
+        const double* kk = p.table.data() + 2 * static_cast<size_t>(p.table_off[k]);
+        for (int j = 0; j < K; ++j) {
+            const double a = kk[2 * j], b = keys0[2 * j];
+            if (a != a ? b == b : std::memcmp(&a, &b, sizeof(double)) != 0) return;
+        }
+    }
+    std::vector<double> it(static_cast<size_t>(K) * (M + 1));
+    for (int j = 0; j < K; ++j) it[j] = keys0[2 * j];
+    for (size_t k = 0; k < M; ++k) {
+        const double* kk = p.table.data() + 2 * static_cast<size_t>(p.table_off[k]);
+        const DevMaterial<double> d = device_material(p, k);
+        for (int j = 0; j < K; ++j)
+            it[K * (k + 1) + j] = p.mats[k].kind == RTPB_TABLE ? kk[2 * j + 1]
+                                                               : material_n<double, false, false>(d, keys0[2 * j], static_cast<const double*>(nullptr));
+    }
+    p.itab.swap(it);
+    p.nkeys = K;
+    p.feat = (p.feat & ~(4 | 8)) | 16;
 }
 
 template <typename T>
@@ -46,22 +106,11 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         o.tol = T(d.tol); o.ap_sq = T(d.ap_sq); o.shell_lo = T(d.shell_lo); o.shell_hi = T(d.shell_hi);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
-    for (size_t k = 0; k < M; ++k) {
-        const rtpb_material& m = p.mats[k];
-        DevMaterial<T> d{};
-        d.kind = m.kind;
-        bool zero = m.kind == RTPB_SELLMEIER;
-        for (int j = 0; j < 6; ++j) {
-            d.c[j] = T(m.c[j]);
-            zero = zero && m.c[j] == 0.0;
-        }
-        if (zero) d.kind = VACUUM;
-        d.table_off = p.table_off[k];
-        d.table_len = m.kind == RTPB_TABLE ? m.table_len : 0;
-        dm[k] = d;
-    }
+    for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);
     auto* tb = reinterpret_cast<T*>(blob.data() + off_table);
     for (size_t k = 0; k < p.table.size(); ++k) tb[k] = T(p.table[k]);
+    auto* it = reinterpret_cast<T*>(blob.data() + p.off_itab);
+    for (size_t k = 0; k < p.itab.size(); ++k) it[k] = T(p.itab[k]);
     return blob;
 }
 
@@ -153,6 +202,7 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
         p->mats.push_back(m);
     }
     if (!p->table.empty()) p->feat |= (p->table.size() / 2 <= static_cast<size_t>(kLdsTablePairs)) ? 4 : 8;
+    if (g_indexed_materials.load()) build_indexed(*p);
     blob_layout<double>(*p);
     *plan_out = p;
     return RTPB_OK;

@@ -74,6 +74,7 @@ struct TraceArgs {
     const DevSurface<double>* __restrict__ surf;
     const DevMaterial<double>* __restrict__ mats;
     const double* __restrict__ table;
+    const double* __restrict__ itab;   // indexed materials: [nkeys keys][(nsurf+1) x nkeys values]
     int64_t n;
     int64_t in_fs;        // SOA input field stride
     int64_t out_ps;       // output plane (slot) stride
@@ -82,6 +83,7 @@ struct TraceArgs {
     uint64_t mask_hi;
     int32_t nsurf;
     int32_t ntable;       // (wavelength, n) pairs in `table`
+    int32_t nkeys;        // keys of `itab` (feat bit 16)
 };
 
 // The trace kernel's launcher for one (input, storage) type pair: picks the kernel variant for the
@@ -94,7 +96,7 @@ extern template hipError_t launch_trace<float, float>(const TraceArgs<float, flo
 extern template hipError_t launch_trace<double, float>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
 extern template hipError_t launch_trace<float, double>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
 // tuning knobs (rtpb_set_tuning, defined in rtpb_trace.hip)
-extern std::atomic<int> g_aos_staging, g_nt_stores, g_waves_per_eu, g_stage_input, g_host_chunk_mib;
+extern std::atomic<int> g_aos_staging, g_nt_stores, g_waves_per_eu, g_stage_input, g_host_chunk_mib, g_indexed_materials;
 
 // Descriptors are read-only for the whole launch: read them through the constant address space so
 // the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.
@@ -200,6 +202,27 @@ __device__ __forceinline__ bool plane_bit(uint64_t lo, uint64_t hi, int p) {
 // stores in one in-order counter (vmcnt), so waiting for a table load also waits for every history
 // store the wave has in flight.
 constexpr int kLdsTablePairs = 256;
+// Indexed materials (rtpb_plan::feat bit 16): when every TABLE material of a plan is tabulated at the
+// same wavelengths (the bundle's distinct wavelengths, as the Python layer lowers them) and no POLY6
+// material is present, the plan also carries n of EVERY material at those K keys, evaluated on the host
+// with the kernel's own material_n (so the values are the ones the kernel would compute).  The kernel
+// then finds each ray's key index once and reads n(material, key) from LDS at every surface, instead of
+// re-evaluating Sellmeier dispersion (three divisions and a square root) and searching tables per
+// surface.  Layout: [K keys][(S+1) x K values]; at most this many doubles.
+constexpr int kLdsIndexedDoubles = 512;
+
+// Index of wavelength wl among the K sorted keys (NaN last, as sort_table orders them; NaN wl finds a NaN
+// key), or -1.  Same matching rule as material_n's TABLE search, so indexed and searched lookups agree.
+__device__ __forceinline__ int key_index(const double* keys, int K, double wl) {
+    if (wl != wl) return (K > 0 && keys[K - 1] != keys[K - 1]) ? K - 1 : -1;
+    int lo = 0, hi = K;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < wl) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < K && keys[lo] == wl) ? lo : -1;
+}
 
 constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 
@@ -357,11 +380,14 @@ struct rtpb_plan {
     std::vector<int32_t> table_off;
     std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
     // kernel features needed: 1 = PerfectLens, 2 = POLY6 material, 4 = TABLE materials whose table fits
-    // the kernel's LDS copy (kLdsTablePairs), 8 = TABLE materials read from global memory
+    // the kernel's LDS copy (kLdsTablePairs), 8 = TABLE materials read from global memory, 16 = indexed
+    // materials (replaces 4 / 8; see kLdsIndexedDoubles)
     int feat = 0;
+    std::vector<double> itab;           // indexed materials: [nkeys keys][(nsurf+1) x nkeys values]
+    int32_t nkeys = 0;
     std::mutex mu;
     void* blob[rtpbi::kMaxDevices] = {};
-    size_t off_mats = 0, off_table = 0, blob_bytes = 0;   // blob layout, fixed at plan creation
+    size_t off_mats = 0, off_table = 0, off_itab = 0, blob_bytes = 0;   // blob layout, fixed at plan creation
 };
 
 namespace rtpbi {

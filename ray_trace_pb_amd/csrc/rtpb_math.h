@@ -258,6 +258,9 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r) {
 // materials (rtpb_plan::feat).
 template <typename T, bool WITH_POLY6 = true, bool WITH_TABLE = true, typename TablePtr>
 RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
+#if defined(RTPB_EXP_NO_MATERIAL)          // experiment only: material evaluation cost (wrong indices)
+    return T(1) + m.c[0] * T(1e-3) + wl * T(1e-9);
+#endif
     switch (m.kind) {
     case CONSTANT:
         return m.c[0];                                               // MAT:72-79

@@ -14,6 +14,7 @@ std::atomic<int> g_nt_stores{1};
 std::atomic<int> g_waves_per_eu{0};
 std::atomic<int> g_stage_input{0};
 std::atomic<int> g_host_chunk_mib{128};
+std::atomic<int> g_indexed_materials{1};          // read at plan creation (rtpb_plan_create)
 }  // namespace rtpbi
 
 namespace {
@@ -44,6 +45,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int in_dtype, int64_t n
         a.surf = reinterpret_cast<const DevSurface<double>*>(blob);
         a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
         a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
+        a.itab = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_itab);
         a.n = n;
         a.in_fs = in_fs;
         a.out_ps = out_ps;
@@ -52,6 +54,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int in_dtype, int64_t n
         a.mask_hi = hi;
         a.nsurf = plan->nsurf;
         a.ntable = static_cast<int32_t>(plan->table.size() / 2);
+        a.nkeys = plan->nkeys;
         return launch_trace<TIN, TS>(a, il, ol, plan->feat, st);
     };
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -335,6 +338,10 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     if (std::strcmp(key, "host_chunk_mib") == 0) {
         if (value < 1 || value > 4096) return fail(RTPB_E_INVALID, "host_chunk_mib must be in [1, 4096]");
         g_host_chunk_mib.store(static_cast<int>(value));
+        return RTPB_OK;
+    }
+    if (std::strcmp(key, "indexed_materials") == 0) {
+        g_indexed_materials.store(value != 0);
         return RTPB_OK;
     }
     if (std::strcmp(key, "waves_per_eu") == 0) {

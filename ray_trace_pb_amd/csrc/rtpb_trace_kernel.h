@@ -61,11 +61,14 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
     constexpr bool kFinal = (STORE & 8) != 0;
     constexpr bool kLens = (FEAT & 1) != 0, kPoly = (FEAT & 2) != 0;
-    constexpr bool kTabLds = (FEAT & 12) == 4, kTabGlobal = (FEAT & 8) != 0;
-    extern __shared__ double lds_table[];                // FEAT bit 2: the plan's (wavelength, n) pairs
-    if constexpr (kTabLds) {
+    constexpr bool kTabLds = (FEAT & 12) == 4, kTabGlobal = (FEAT & 8) != 0, kIdx = (FEAT & 16) != 0;
+    extern __shared__ double lds_table[];                // FEAT bit 2: the plan's (wavelength, n) pairs;
+                                                         // FEAT bit 4: the indexed-material table
+    if constexpr (kTabLds || kIdx) {
         // before any wave can leave: the unstaged variants run four-wave workgroups and need the barrier
-        for (int k = threadIdx.x; k < 2 * a.ntable; k += kB) lds_table[k] = a.table[k];
+        const int cnt = kIdx ? a.nkeys * (a.nsurf + 2) : 2 * a.ntable;
+        const double* src = kIdx ? a.itab : a.table;
+        for (int k = threadIdx.x; k < cnt; k += kB) lds_table[k] = src[k];
         if constexpr (kB > 64) __syncthreads();
     }
     // per wave: "at" and "after" tiles of 64 records (4 KiB f64, 2 KiB f32: the LDS budget allows 5 f64 /
@@ -116,9 +119,18 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
     const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
     const cptr<T> table = (cptr<T>)(a.table);
+    // indexed materials: the ray's key once (-1 = wavelength not among the plan's keys: every material
+    // is then evaluated as without the index, TABLE materials giving NaN as a table miss does)
+    const int widx = kIdx ? key_index(lds_table, a.nkeys, wl0) : -1;
     auto mat_n = [&](cptr<DevMaterial<T>> mp) -> T {
-        if constexpr (kTabLds) return material_n<T, kPoly, true>(load_material<T>(mp), wl0, lds_table);
-        else return material_n<T, kPoly, kTabGlobal>(load_material<T>(mp), wl0, table);
+        if constexpr (kIdx) {
+            if (widx >= 0) return lds_table[a.nkeys * (1 + static_cast<int>(mp - mats)) + widx];
+            return material_n<T, false, false>(load_material<T>(mp), wl0, table);
+        } else if constexpr (kTabLds) {
+            return material_n<T, kPoly, true>(load_material<T>(mp), wl0, lds_table);
+        } else {
+            return material_n<T, kPoly, kTabGlobal>(load_material<T>(mp), wl0, table);
+        }
     };
     if constexpr (kFinal) {
         T n_cur = mat_n(mats);
@@ -202,7 +214,8 @@ template <typename TI, typename T, int IL, int OL, int ST, int W, int FEAT>
 hipError_t launch_w(const TraceArgs<TI, T>& a, hipStream_t st) {
     constexpr int kB = trace_block(OL, ST);
     const int64_t blocks = (a.n + kB - 1) / kB;
-    const size_t lds = (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
+    const size_t lds = (FEAT & 16)        ? static_cast<size_t>(a.nkeys) * (a.nsurf + 2) * sizeof(double)
+                       : (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
 #if defined(RTPB_EXP_PERSIST)
     static int resident = 0;                     // experiment: one wave slot per workgroup of the grid
     if (!resident) {
@@ -241,6 +254,8 @@ hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
     case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
     case 4: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(4), 4>(a, st);
     case 5: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(5), 5>(a, st);
+    case 16: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(16), 16>(a, st);
+    case 17: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(17), 17>(a, st);
     default: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(15), 15>(a, st);   // POLY6 or a large table: everything in
     }
 #undef RTPB_WPE
