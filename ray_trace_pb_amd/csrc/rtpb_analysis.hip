@@ -111,6 +111,7 @@ struct SweepArgs {
     const double* __restrict__ table;
     const double2* __restrict__ tab;    // (cos, sin): thetas [n_thetas], then phis [nphis]
     const double* __restrict__ grp;     // per group: x, y, z, wavelength
+    const double* __restrict__ gn;      // FEAT bit 4: per group, n of the S+1 materials at its wavelength
     double* __restrict__ partials;
     int64_t n_thetas, nphis, gsize, tiles;
     double c[3], ex[3], ey[3];
@@ -152,9 +153,16 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     const cptr<double> table = (cptr<double>)(a.table);
     const double wl0 = rA.wl;                          // one wavelength per group
     const Rcp<double> iwl = make_rcp(wl0);             // shared divisor of every phase update
-    double n_cur = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats), wl0, table);
+    // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the
+    // kernel's own material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
+    const cptr<double> gn = (cptr<double>)(a.gn) + g * (a.nsurf + 1);
+    auto mat_n = [&](int k) -> double {
+        if constexpr ((FEAT & 16) != 0) return gn[k];
+        else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
+    };
+    double n_cur = mat_n(0);
     for (int s = 0; s < a.nsurf; ++s) {
-        const double n_next = material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + s + 1), wl0, table);
+        const double n_next = mat_n(s + 1);
         const DevSurface<double> sd = load_surface<double>(surf + s);
         Ray<double> aA, aB;
         propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, iwl, iwl, aA, aB);
@@ -301,8 +309,14 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     rc = plan_device_blob(plan, device, &blob);
     if (rc) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // one upload: trig tables then the per-group parameters
-    const size_t ntab = size_t(n_thetas + nphis), bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double);
+    // one upload: trig tables, the per-group parameters, and (no POLY6 material) every material's n at
+    // each group's wavelength -- material_n on the host, i.e. the kernel's own arithmetic (-ffp-contract=
+    // off, IEEE division and sqrt), at the wavelength the kernel would see (rounded to the storage type)
+    const bool pre_n = (plan->feat & 2) == 0;
+    const size_t M = plan->mats.size();
+    const size_t ntab = size_t(n_thetas + nphis);
+    const size_t bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) +
+                         (pre_n ? size_t(n_groups) * M * sizeof(double) : 0);
     void* dbuf = nullptr;
     HIP_TRY(hipMallocAsync(&dbuf, bytes, st));
     PinnedStaging& g_pinned = pinned_staging();
@@ -311,6 +325,17 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     std::memcpy(g_pinned.buf, theta_cos_sin, size_t(2 * n_thetas) * sizeof(double));
     std::memcpy(g_pinned.buf + 2 * n_thetas, phi_cos_sin, size_t(2 * nphis) * sizeof(double));
     std::memcpy(g_pinned.buf + 2 * ntab, group_params, size_t(4 * n_groups) * sizeof(double));
+    if (pre_n) {
+        double* gn = g_pinned.buf + 2 * ntab + 4 * n_groups;
+        std::vector<DevMaterial<double>> dm(M);
+        for (size_t k = 0; k < M; ++k) dm[k] = device_material(*plan, k);
+        for (int64_t gi = 0; gi < n_groups; ++gi) {
+            const double w = group_params[4 * gi + 3];
+            const double wl = plan->dtype == RTPB_F32 ? double(float(w)) : w;
+            for (size_t k = 0; k < M; ++k)
+                gn[gi * M + k] = material_n<double, false, true>(dm[k], wl, plan->table.data());
+        }
+    }
     rc = g_pinned.upload(dbuf, bytes, st);
     if (rc) return rc;
     SweepArgs a{};
@@ -319,6 +344,7 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
     a.tab = static_cast<const double2*>(dbuf);
     a.grp = reinterpret_cast<const double*>(static_cast<char*>(dbuf) + ntab * sizeof(double2));
+    a.gn = a.grp + 4 * n_groups;
     a.partials = workspace;
     a.n_thetas = n_thetas;
     a.nphis = nphis;
@@ -332,7 +358,9 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     auto go = [&](auto tag) {
         using TS = decltype(tag);
         const int f = plan->feat & 3;                 // lens / POLY6 code; tables are always compiled in here
-        if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
+        if (pre_n && f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16>), grid, dim3(kBlock), 0, st, a);
+        else if (pre_n) hipLaunchKernelGGL((sweep_kernel<TS, 17>), grid, dim3(kBlock), 0, st, a);
+        else if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
         else if (f == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
         else hipLaunchKernelGGL((sweep_kernel<TS, 3>), grid, dim3(kBlock), 0, st, a);
     };

@@ -393,6 +393,8 @@ struct rtpb_plan {
 namespace rtpbi {
 // Device copy of a plan's descriptors (created on first use per device, then immutable).
 int plan_device_blob(rtpb_plan* p, int dev, void** out);
+// The device material descriptor of plan material k, as the kernels see it (zero Sellmeier = VACUUM).
+DevMaterial<double> device_material(const rtpb_plan& p, size_t k);
 // RTPB_OK, or RTPB_E_NODEV with the message set.
 int check_device(int dev);
 }  // namespace rtpbi

@@ -23,8 +23,14 @@ def main():
     ap.add_argument("--nphis", type=int, default=3162)
     ap.add_argument("--dtype", default="float64")
     ap.add_argument("--devices", default="", help="in-process multi-GPU: 'all' or comma-separated GPU ids")
+    ap.add_argument("--warmup", type=int, default=1,
+                    help="untimed small sweeps first (plan creation, code-object load on first launch)")
+    ap.add_argument("--lib", default="", help="library build to load instead of the in-tree librtpb.so (A/B)")
     args = ap.parse_args()
     import torch
+    if args.lib:
+        from ray_trace_pb_amd import _capi
+        _capi.LIB_PATH = os.path.abspath(args.lib)
     import ray_trace_pb_amd.materials as mat
     import ray_trace_pb_amd.raytrace as rt
     from ray_trace_pb_amd import analysis
@@ -42,13 +48,16 @@ def main():
     system = systems.c5_system(rt, mat)
     wls = systems.C5_WAVELENGTHS
     theta = 0.5 * np.pi / 180
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
     devices = None
     if args.devices:
         devices = list(range(torch.cuda.device_count())) if args.devices == "all" else \
             [int(d) for d in args.devices.split(",")]
+    for _ in range(args.warmup):
+        analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine, wls, theta, 33, 32, device=dev,
+                            dtype=args.dtype, devices=devices)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
     summ, timing = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine, wls, theta, args.n_thetas,
                                        args.nphis, device=dev, dtype=args.dtype, devices=devices)
     if world > 1:
