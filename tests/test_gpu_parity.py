@@ -144,6 +144,19 @@ def test_sharded_host_trace_is_bitwise_equal():
     assert np.array_equal(got3, ref, equal_nan=True)
 
 
+@pytest.mark.parametrize("name", [c for c in CASES if c.startswith("fuzz_")])
+def test_fuzz_sharded_host_trace_and_float32_storage(name):
+    """The seeded random systems through rtpb_trace_host split over three shards of GPU 0 (host threads,
+    chunked pipeline), float64 and float32 storage, all and final planes: the reference's history
+    (rounded once for float32) bit for bit."""
+    system, m0, m1, rays, ref = build_case(name)
+    assert np.array_equal(system.ray_trace(rays, m0, m1, devices=[0, 0, 0]), ref, equal_nan=True)
+    got32 = system.ray_trace(rays, m0, m1, dtype="float32", devices=[0, 0, 0])
+    assert np.array_equal(got32, ref.astype(np.float32), equal_nan=True)
+    fin = system.ray_trace(rays, m0, m1, planes="final", devices=[0, 0])
+    assert np.array_equal(fin, ref[-1:], equal_nan=True)
+
+
 def test_user_material_subclass_lowers_to_table():
     """A Material subclass overriding n() (the reference's plugin point) traces on the GPU via a
     per-wavelength table, bit-identical to evaluating its n() per ray."""
