@@ -104,6 +104,7 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         }
         o.R = T(d.R); o.R2 = T(d.R2); o.absR = T(d.absR); o.ap = T(d.ap); o.f = T(d.f); o.sin_a = T(d.sin_a);
         o.tol = T(d.tol); o.ap_sq = T(d.ap_sq); o.shell_lo = T(d.shell_lo); o.shell_hi = T(d.shell_hi);
+        o.rR = T(d.rR); o.rf = T(d.rf); o.rcp_ok = d.rcp_ok;
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);

@@ -87,14 +87,27 @@ template <typename T> RTPB_HD bool is_nan(T v) { return v != v; }
 #define RTPB_FASTSQRT 1
 #endif
 
-template <typename T> RTPB_HD T tsqrt(T v);
+// Guard policies of the exact fast paths below.  Each shortcut is exact only inside a range of its
+// operands; outside it the operation must take the compiler's full sequence.
+//   GuardBranch: a per-operation branch to the full sequence (default; the all-planes history kernels).
+//   GuardDefer:  no branch -- the operation only records that a lane left the range (g->bad); the caller
+//                re-traces such rays with GuardBranch afterwards.  Removing the per-operation branches
+//                lets the compiler schedule a whole surface as one block (final-plane kernels and the
+//                spot sweep: -20 % and more).
+struct GuardBranch { static constexpr bool kDefer = false; };
+struct GuardDefer { static constexpr bool kDefer = true; bool bad = false; };
+
 // gfx950 has no f64 sqrt instruction: the compiler emits (i) x < 2^-767 ? x * 2^256 : x, (ii) rsq + two
 // Goldschmidt/Newton rounds (mul, mul, 7 fma), (iii) the inverse rescale, and (iv) a select that returns
 // x itself for +-0 and +inf -- 18 instructions.  For 2^-767 <= x < inf, for x < 0 and for NaN, steps (i),
 // (iii) and (iv) are identities (a negative or NaN x gives NaN either way), so the device path runs step
 // (ii) alone -- the identical instructions, hence identical bits -- and hands the remaining inputs
 // (+-0, denormals, tiny normals, +inf) to the full expansion.
-template <> RTPB_HD double tsqrt<double>(double v) {
+template <typename T, class G = GuardBranch>
+RTPB_HD T tsqrt(T v, G* g = nullptr) {
+    if constexpr (sizeof(T) != 8) {
+        return sqrtf(v);
+    } else {
 #if defined(RTPB_FASTSQRT)
     const double y = __builtin_amdgcn_rsq(v);
     const double s0 = v * y;
@@ -106,13 +119,24 @@ template <> RTPB_HD double tsqrt<double>(double v) {
     const double s2 = __builtin_fma(d0, h1, s1);
     const double d1 = __builtin_fma(-s2, s2, v);
     double s3 = __builtin_fma(d1, h1, s2);
-    if (__builtin_expect((v >= 0.0 && v < 0x1p-767) || v == __builtin_inf(), 0)) s3 = sqrt(v);
+    const bool slow = (v >= 0.0 && v < 0x1p-767) || v == __builtin_inf();
+    if constexpr (G::kDefer) {
+        // +-0 and +inf (normal incidence gives sqrt(0) on every axial ray) are their own square roots:
+        // a select, so only 0 < v < 2^-767 is left to the re-trace
+        if (v == 0.0 || v == __builtin_inf()) s3 = v;
+        g->bad = g->bad || (v > 0.0 && v < 0x1p-767);
+    } else {
+#if !defined(RTPB_EXP_NO_GUARDS)           // experiment only: the cost of the range guards (inexact)
+        if (__builtin_expect(slow, 0)) s3 = sqrt(v);
+#endif
+    }
     return s3;
 #else
+    (void)g;
     return sqrt(v);
 #endif
+    }
 }
-template <> RTPB_HD float tsqrt<float>(float v) { return sqrtf(v); }
 
 template <typename T> RTPB_HD T tabs(T v) { return v < T(0) ? -v : (v == T(0) ? T(0) : v); }
 
@@ -209,46 +233,70 @@ RTPB_HD Rcp<T> make_rcp(T b) {
 }
 
 // a / r.b
-template <typename T>
-RTPB_HD T div1(T a, const Rcp<T>& r) {
+template <typename T, class G = GuardBranch>
+RTPB_HD T div1(T a, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, r.b, r.y);
-        if (__builtin_expect(!(r.ok && fastdiv_num_ok(a)), 0)) q = a / r.b;
+        const bool slow = !(r.ok && fastdiv_num_ok(a));
+        if constexpr (G::kDefer) {
+            g->bad = g->bad || slow;
+        } else {
+#if !defined(RTPB_EXP_NO_GUARDS)
+            if (__builtin_expect(slow, 0)) q = a / r.b;
+#endif
+        }
         return q;
     }
 #endif
+    (void)g;
     return a / r.b;
 }
 
 // a / b where r = make_rcp(b0) and b is b0 or NaN (a wavelength after its row was killed): a NaN b gives
 // NaN either way (div_fixup / the division), so y of b0 serves every value b can take
-template <typename T>
-RTPB_HD T div1_as(T a, T b, const Rcp<T>& r) {
+template <typename T, class G = GuardBranch>
+RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, b, r.y);
-        if (__builtin_expect(!(r.ok && fastdiv_num_ok(a)), 0)) q = a / b;
+        const bool slow = !(r.ok && fastdiv_num_ok(a));
+        if constexpr (G::kDefer) {
+            g->bad = g->bad || slow;
+        } else {
+#if !defined(RTPB_EXP_NO_GUARDS)
+            if (__builtin_expect(slow, 0)) q = a / b;
+#endif
+        }
         return q;
     }
 #endif
+    (void)g;
     return a / b;
 }
 
 // (x, y, z) / r.b, one guard for the three quotients
-template <typename T>
-RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r) {
+template <typename T, class G = GuardBranch>
+RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
-        if (__builtin_expect(!(r.ok && fastdiv_num_ok(x) && fastdiv_num_ok(y) && fastdiv_num_ok(z)), 0)) {
-            x = x / r.b; y = y / r.b; z = z / r.b;
+        const bool slow = !(r.ok && fastdiv_num_ok(x) && fastdiv_num_ok(y) && fastdiv_num_ok(z));
+        if constexpr (G::kDefer) {
+            g->bad = g->bad || slow;
         } else {
-            x = qx; y = qy; z = qz;
+#if !defined(RTPB_EXP_NO_GUARDS)
+            if (__builtin_expect(slow, 0)) {
+                x = x / r.b; y = y / r.b; z = z / r.b;
+                return;
+            }
+#endif
         }
+        x = qx; y = qy; z = qz;
         return;
     }
 #endif
+    (void)g;
     x = x / r.b; y = y / r.b; z = z / r.b;
 }
 
@@ -256,8 +304,8 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r) {
 // WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
 // budget); WITH_TABLE = false compiles the TABLE case out.  Either is only valid for plans without such
 // materials (rtpb_plan::feat).
-template <typename T, bool WITH_POLY6 = true, bool WITH_TABLE = true, typename TablePtr>
-RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
+template <typename T, bool WITH_POLY6 = true, bool WITH_TABLE = true, typename TablePtr, class G = GuardBranch>
+RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table, G* g = nullptr) {
 #if defined(RTPB_EXP_NO_MATERIAL)          // experiment only: material evaluation cost (wrong indices)
     return T(1) + m.c[0] * T(1e-3) + wl * T(1e-9);
 #endif
@@ -272,7 +320,7 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
     case SELLMEIER: {                                                // MAT:48-51
         const T w2 = wl * wl;
         const T acc = m.c[0] * w2 / (w2 - m.c[3]) + m.c[1] * w2 / (w2 - m.c[4]) + m.c[2] * w2 / (w2 - m.c[5]);
-        return tsqrt<T>(acc + T(1));
+        return tsqrt<T>(acc + T(1), g);
     }
     case POLY6: {                                                    // MAT:137-144 (Ebaf11)
         if constexpr (!WITH_POLY6) {
@@ -281,7 +329,7 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
             const T w2 = wl * wl;
             const T n2 = m.c[0] + m.c[1] * w2 + m.c[2] * tpow<T>(wl, T(-2)) + m.c[3] * tpow<T>(wl, T(-4)) +
                          m.c[4] * tpow<T>(wl, T(-6)) + m.c[5] * tpow<T>(wl, T(-8));
-            return tsqrt<T>(n2);
+            return tsqrt<T>(n2, g);
         }
     }
     default: {                                                       // TABLE: host-evaluated n(lambda)
@@ -307,12 +355,12 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table) {
 // ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
 // iden: optional make_rcp of the denominator d.nrm, shared by several planes with the same normal.
-template <typename T>
+template <typename T, class G = GuardBranch>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
-                        const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr) {
+                        const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr, G* g = nullptr) {
     const T num = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz);
     const T den = r.dx * nx + r.dy * ny + r.dz * nz;
-    const T t = iden ? div1_as(num, den, *iden) : num / den;
+    const T t = iden ? div1_as(num, den, *iden, g) : num / den;
     const T s = t < T(0) ? T(-1) : T(1);
     const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
     Ray<T> o;
@@ -320,8 +368,8 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     o.y = r.y + vy;
     o.z = r.z + vz;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
-    const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz);
-    o.ph = r.ph + div1_as(dist * s * T(2) * T(Const<T>::pi), r.wl, iwl) * n;
+    const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
+    o.ph = r.ph + div1_as(dist * s * T(2) * T(Const<T>::pi), r.wl, iwl, g) * n;
     o.wl = r.wl;
     if (exclude_backward && s == T(-1)) kill(o);
     if (t_out) *t_out = t;
@@ -329,12 +377,12 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
 }
 
 // ------------------------------------------------------------------ SphericalSurface.get_intersect (RT:1479-1516)
-template <typename T>
-RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl) {
+template <typename T, class G = GuardBranch>
+RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr) {
     const T ox = r.x - s.c[0], oy = r.y - s.c[1], oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ox * ox + oy * oy + oz * oz - s.R2;
-    const T root = tsqrt<T>(B * B - T(4) * C);
+    const T root = tsqrt<T>(B * B - T(4) * C, g);
     T t1 = T(0.5) * (-B + root);
     T t2 = T(0.5) * (-B - root);
     const T inf = T(1) / T(0);
@@ -348,8 +396,8 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     o.z = r.z + r.dz * t;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
-    const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz);
-    o.ph = r.ph + div1_as(dist * T(2) * T(Const<T>::pi), r.wl, iwl) * n;
+    const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz, g);
+    o.ph = r.ph + div1_as(dist * T(2) * T(Const<T>::pi), r.wl, iwl, g) * n;
     o.wl = r.wl;
     return o;
 }
@@ -364,10 +412,10 @@ RTPB_HD bool positive_finite(T v) {
 }
 
 // v / |v| with NaN components replaced by 0 (RT:1203-1209)
-template <typename T>
-RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
-    const T nrm = tsqrt<T>(x * x + y * y + z * z);
-    div3(x, y, z, make_rcp(nrm));
+template <typename T, class G = GuardBranch>
+RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
+    const T nrm = tsqrt<T>(x * x + y * y + z * z, g);
+    div3(x, y, z, make_rcp(nrm), g);
     // A NaN quotient needs a zero, infinite or NaN norm: when 0 < |v| < inf every component is finite and
     // every quotient a number, so one class test skips the three per-component fix-ups (normal incidence,
     // dead rows and garbage input take them)
@@ -379,26 +427,26 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z) {
 }
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
-template <typename T>
-RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz) {
+template <typename T, class G = GuardBranch>
+RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
     T bx = ri.dy * Nz - ri.dz * Ny;
     T by = ri.dz * Nx - ri.dx * Nz;
     T bz = ri.dx * Ny - ri.dy * Nx;
-    unit_or_zero(bx, by, bz);
+    unit_or_zero(bx, by, bz, g);
     cx = Ny * bz - Nz * by;
     cy = Nz * bx - Nx * bz;
     cz = Nx * by - Ny * bx;
-    unit_or_zero(cx, cy, cz);
+    unit_or_zero(cx, cy, cz, g);
 }
 
 // Snell refraction of the intersected ray (RT:1197-1221)
-template <typename T>
-RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2) {
+template <typename T, class G = GuardBranch>
+RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz);
+    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = n1 / n2 * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
     const T sgn = np_sign<T>(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
-    const T tang = sgn * tsqrt<T>(T(1) - mag * mag);
+    const T tang = sgn * tsqrt<T>(T(1) - mag * mag, g);
     Ray<T> o;
     o.dx = mag * cx + tang * Nx;
     o.dy = mag * cy + tang * Ny;
@@ -413,10 +461,10 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2) {
 }
 
 // law of reflection (RT:1267-1289)
-template <typename T>
-RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz) {
+template <typename T, class G = GuardBranch>
+RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz);
+    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag_na = -(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
     const T mag_nc = cx * ri.dx + cy * ri.dy + cz * ri.dz;
     Ray<T> o;
@@ -462,64 +510,66 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
 // One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
-template <typename T, int KIND, typename EmitAt>
+template <typename T, int KIND, typename EmitAt, class G = GuardBranch>
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
-                          Ray<T>& after) {
+                          Ray<T>& after, G* g = nullptr) {
     if constexpr (KIND == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
         // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
         const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
-        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden));   // RT:1790-1793
+        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden, g));   // RT:1790-1793
         const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
         const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
-        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden);
+        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
-        const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz);
-        if (spn > T(1e-12)) div3(spx, spy, spz, make_rcp(spn));
+        const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz, g);
+        if (spn > T(1e-12)) div3(spx, spy, spz, make_rcp(spn), g);
         const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
-        const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z);
+        const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z, g);
         T ux = r1x, uy = r1y, uz = r1z;
-        if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n));
+        if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n), g);
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
         o.x = n1 * f * sin_t1 * spx + Bx;
         o.y = n1 * f * sin_t1 * spy + By;
         o.z = n1 * f * sin_t1 * spz + Bz;
-        const T sin_t2 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0)) / n2;
-        const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2);
+        const T sin_t2 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g) / n2;
+        const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
         o.dz = sin_t2 * uz + cos_t2 * nz;
         o.wl = r.wl;
         if (tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a) kill(o);
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
-        const T k = div1_as(T(Const<T>::two_pi), r.wl, iwl);
+        const T k = div1_as(T(Const<T>::two_pi), r.wl, iwl, g);
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
-        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl);
+        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
+                         static_cast<const Rcp<T>*>(nullptr), g);
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
         if constexpr (KIND == SPHERE) {
-            ri = sphere_hit(r, s, n1, iwl);
+            ri = sphere_hit(r, s, n1, iwl, g);
             Nx = ri.x - s.c[0];                                            // (p - c) / R, RT:1476
             Ny = ri.y - s.c[1];
             Nz = ri.z - s.c[2];
-            div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0));
+            div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl);   // RT:1331-1337, 1398-1403
+            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
+                          static_cast<const Rcp<T>*>(nullptr), g);                  // RT:1331-1337, 1398-1403
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
-            after = reflect(ri, Nx, Ny, Nz);
+            after = reflect(ri, Nx, Ny, Nz, g);
             if (!on_flat(ri, s)) kill(after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
             if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
             emit_at(ri);
-            after = snell(ri, Nx, Ny, Nz, n1, n2);
+            after = snell(ri, Nx, Ny, Nz, n1, n2, g);
             const bool ok = (KIND == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
             if (!ok) kill(after);
         }
@@ -529,35 +579,36 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
 // Any surface: a wave-uniform switch on the kind.  WITH_LENS = false compiles the PerfectLens case out
 // (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans without PerfectLens
 // surfaces (rtpb_plan::feat).
-template <typename T, bool WITH_LENS = true, typename EmitAt>
+template <typename T, bool WITH_LENS = true, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
-                                    EmitAt&& emit_at, Ray<T>& after) {
+                                    EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
     const int kind = s.kind;
-    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, iwl, emit_at, after);
-    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, iwl, emit_at, after);
-    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, iwl, emit_at, after);
-    else surface_step<T, FLAT>(s, r, n1, n2, iwl, emit_at, after);
+    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, iwl, emit_at, after, g);
+    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, iwl, emit_at, after, g);
+    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, iwl, emit_at, after, g);
+    else surface_step<T, FLAT>(s, r, n1, n2, iwl, emit_at, after, g);
 }
 
 // Two independent rays through the same surface: one kind dispatch, both bodies in one straight-line
 // region so the scheduler can interleave their dependency chains.
-template <typename T, bool WITH_LENS = true>
+template <typename T, bool WITH_LENS = true, class G = GuardBranch>
 RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, const Ray<T>& rb, T n1, T n2,
-                                    const Rcp<T>& iwl_a, const Rcp<T>& iwl_b, Ray<T>& after_a, Ray<T>& after_b) {
+                                    const Rcp<T>& iwl_a, const Rcp<T>& iwl_b, Ray<T>& after_a, Ray<T>& after_b,
+                                    G* g = nullptr) {
     auto none = [](const Ray<T>&) {};
     const int kind = s.kind;
     if (WITH_LENS && kind == PERFECT_LENS) {
-        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, iwl_a, none, after_a);
-        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, iwl_b, none, after_b);
+        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, iwl_a, none, after_a, g);
+        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, iwl_b, none, after_b, g);
     } else if (kind == SPHERE) {
-        surface_step<T, SPHERE>(s, ra, n1, n2, iwl_a, none, after_a);
-        surface_step<T, SPHERE>(s, rb, n1, n2, iwl_b, none, after_b);
+        surface_step<T, SPHERE>(s, ra, n1, n2, iwl_a, none, after_a, g);
+        surface_step<T, SPHERE>(s, rb, n1, n2, iwl_b, none, after_b, g);
     } else if (kind == PLANE_MIRROR) {
-        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, iwl_a, none, after_a);
-        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, iwl_b, none, after_b);
+        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, iwl_a, none, after_a, g);
+        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, iwl_b, none, after_b, g);
     } else {
-        surface_step<T, FLAT>(s, ra, n1, n2, iwl_a, none, after_a);
-        surface_step<T, FLAT>(s, rb, n1, n2, iwl_b, none, after_b);
+        surface_step<T, FLAT>(s, ra, n1, n2, iwl_a, none, after_a, g);
+        surface_step<T, FLAT>(s, rb, n1, n2, iwl_b, none, after_b, g);
     }
 }
 

@@ -50,8 +50,13 @@ constexpr int trace_block(int out_layout, int store) {
 // without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
 // table lookup the surface loop never waits on the vmcnt counter, which on gfx950 would also wait for
 // every history store in flight (see kLdsTablePairs).  rtpb_plan::feat picks the variant.
+#if defined(RTPB_EXP_MAXW)                  // experiment only: cap the waves per SIMD of the history kernels
+#define RTPB_MAXW(ST) (((ST) & 8) ? 8 : RTPB_EXP_MAXW)
+#else
+#define RTPB_MAXW(ST) 8
+#endif
 template <typename TIN, typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
-__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, RTPB_MAXW(STORE))))
 void trace_kernel(TraceArgs<TIN, TS> a) {
     constexpr int kB = trace_block(OUT_LAYOUT, STORE);
     using T = double;
@@ -138,7 +143,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             const T n_next = mat_n(mats + s + 1);
             Ray<T> after;
             propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
-                                                         [](const Ray<T>&) {}, after);
+                                             [](const Ray<T>&) {}, after);
             r = after;
             n_cur = n_next;
         }

@@ -13,9 +13,13 @@ using namespace rtpb;
 
 namespace {
 
+constexpr int kOut = 19;
+
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
-//      [8] div1(a, host_rcp(b, yh)) with yh = the host's RN(1 / b) (the descriptors' rR / rf)
+//      [8] div1(a, host_rcp(b, yh)) with yh = the host's RN(1 / b) (the descriptors' rR / rf),
+//      then the GuardDefer forms (no fallback branch; a flag instead): [9] div1, [10] its flag,
+//      [11..13] div3, [14] its flag, [15] tsqrt(b), [16] its flag, [17] div1_as, [18] its flag
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -36,6 +40,19 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     const double mb = fabs(bi);          // host_rcp_ok (rtpb_math.h), the flag lower_surface stores
     const bool ok = (mb >= 0x1p-120 && mb <= 0x1p120) || bi == 0.0 || isinf(bi) || isnan(bi);
     out[8 * n + i] = div1(ai, host_rcp(bi, yh[i], ok));
+    GuardDefer g1, g2, g3, g4;
+    out[9 * n + i] = div1(ai, r, &g1);
+    out[10 * n + i] = g1.bad ? 1.0 : 0.0;
+    double dx = ai, dy = a2[i], dz = a3[i];
+    div3(dx, dy, dz, r, &g2);
+    out[11 * n + i] = dx;
+    out[12 * n + i] = dy;
+    out[13 * n + i] = dz;
+    out[14 * n + i] = g2.bad ? 1.0 : 0.0;
+    out[15 * n + i] = tsqrt<double>(bi, &g3);
+    out[16 * n + i] = g3.bad ? 1.0 : 0.0;
+    out[17 * n + i] = div1_as(ai, bb, r, &g4);
+    out[18 * n + i] = g4.bad ? 1.0 : 0.0;
 }
 
 }  // namespace
@@ -54,13 +71,13 @@ extern "C" int fastdiv_check(const double* a, const double* a2, const double* a3
     }
     if (e == hipSuccess) e = hipMalloc(&dk, static_cast<size_t>(n));
     if (e == hipSuccess) e = hipMemcpy(dk, kill, static_cast<size_t>(n), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&dout, 9 * bytes);
+    if (e == hipSuccess) e = hipMalloc(&dout, kOut * bytes);
     if (e == hipSuccess) {
         check_kernel<<<static_cast<unsigned>((n + 255) / 256), 256>>>(dev[0], dev[1], dev[2], dev[3], dev[4], dk, n,
                                                                       dout);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpy(out, dout, 9 * bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, kOut * bytes, hipMemcpyDeviceToHost);
     for (double* p : dev) (void)hipFree(p);
     (void)hipFree(dk);
     (void)hipFree(dout);

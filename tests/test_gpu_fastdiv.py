@@ -33,6 +33,14 @@ def _check(a, a2, a3, b, kill):
         _same(out[6], np.sqrt(b))        # tsqrt
         _same(out[7], np.sqrt(a))
         _same(out[8], a / b)             # div1 with the host's reciprocal (descriptor rR / rf)
+        # GuardDefer: no fallback branch; where the flag is clear the value is the exact one, and the
+        # flag is set only where an operand left the shortcut's exact range (the flagged rays are re-traced)
+        for val, flag, exp in ((out[9], out[10], a / b), (out[11], out[14], a / b), (out[12], out[14], a2 / b),
+                               (out[13], out[14], a3 / b), (out[15], out[16], np.sqrt(b)),
+                               (out[17], out[18], a / bb)):
+            ok = flag == 0
+            _same(val[ok], exp[ok])
+        return out
 
 
 def _rand_bits(rng, n):
@@ -78,6 +86,23 @@ def test_fastdiv_specials():
     a2, a3 = np.roll(a, 1), np.roll(a, 2)
     kill = (np.arange(a.size) % 3 == 0)
     _check(a, a2, a3, b, kill)
+
+
+def test_deferred_guards_flag_only_out_of_range_operands():
+    """Ordinary operands (the magnitudes a trace produces, zeros and infinities included) are never
+    flagged by the GuardDefer forms: the final-plane kernels re-trace only pathological rays."""
+    rng = np.random.default_rng(11)
+    n = 200_000
+    a = _pow2_band(rng, n, -300, 300)
+    b = _pow2_band(rng, n, -100, 100)
+    a[::97] = 0.0
+    b[::89] = 0.0
+    a[::101] = np.inf
+    b[::103] = np.inf
+    kill = np.zeros(n, dtype=np.uint8)
+    out = _check(a, a * 0.5, -a, b, kill)
+    for f in (10, 14, 16, 18):
+        assert not out[f].any(), (f, int(out[f].sum()))
 
 
 def test_fastdiv_normalisation_inputs():
