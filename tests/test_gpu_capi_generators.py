@@ -1,0 +1,67 @@
+"""C-ABI entry points the Python layer does not call (it uses the bit-exact *_tables forms):
+rtpb_ray_fan / rtpb_collimated_rays evaluate cos/sin with the device libm -- within 1 ulp of the host's
+(include/rtpb.h), so they agree with the reference generators (RT:45-161) to a few ulps with identical
+ray order and exactly equal non-trigonometric fields -- and rtpb_shutdown, after which the library
+brings its device state back on the next call."""
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from ray_trace_pb_amd import _capi as C  # noqa: E402
+from ray_trace_pb_amd import _engine as E  # noqa: E402
+import systems  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _d3(v):
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+@pytest.mark.parametrize("dtype", [C.RTPB_F64, C.RTPB_F32])
+def test_device_trig_ray_fan_close_to_reference_generator(dtype):
+    pt, th, nt, nph, wl = [0.5, -0.25, 1.0], 0.3, 101, 64, 0.635
+    c = systems.unit([0.0, 0.6, 0.8])
+    ref = rt.get_ray_fan(pt, th, nt, wl, nphis=nph, center_ray=tuple(c))
+    tdt = torch.float64 if dtype == C.RTPB_F64 else torch.float32
+    out = torch.empty((nt * nph, 8), dtype=tdt, device=DEV)
+    C.check(C.lib().rtpb_ray_fan(0, dtype, out.data_ptr(), _d3(pt), th, nt, nph, _d3(c), wl,
+                                 torch.cuda.current_stream(DEV).cuda_stream))
+    got = out.double().cpu().numpy()
+    assert got.shape == ref.shape
+    tol = 4e-16 if dtype == C.RTPB_F64 else 1.2e-7
+    np.testing.assert_allclose(got[:, :6], ref[:, :6].astype(np.float32 if tdt == torch.float32 else np.float64),
+                               rtol=0, atol=tol * 4)
+    assert np.array_equal(got[:, 6:], ref[:, 6:].astype(np.float32).astype(np.float64) if tdt == torch.float32
+                          else ref[:, 6:])
+
+
+def test_device_trig_collimated_rays_close_to_reference_generator():
+    pt, dmax, nd, nph, phi0, wl = [0.0, 1.0, -2.0], 3.0, 41, 16, 0.3, 0.5
+    normal = systems.unit([np.sin(0.2), 0.0, np.cos(0.2)])
+    ref = rt.get_collimated_rays(pt, dmax, nd, wl, nphis=nph, phi_start=phi0, normal=normal)
+    out = torch.empty((nd * nph, 8), dtype=torch.float64, device=DEV)
+    C.check(C.lib().rtpb_collimated_rays(0, C.RTPB_F64, out.data_ptr(), _d3(pt), dmax, nd, nph, phi0, _d3(normal), wl,
+                                         torch.cuda.current_stream(DEV).cuda_stream))
+    got = out.cpu().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-14)
+    assert np.array_equal(got[:, 3:], ref[:, 3:])            # directions, phase, wavelength: no trig
+
+
+def test_shutdown_then_trace_again():
+    system, rays, m0, m1 = systems.c1_plano_convex(rt, mat)
+    before = system.ray_trace(rays, m0, m1)
+    torch.cuda.synchronize()
+    E.clear_plan_cache()                                      # plans must be destroyed first
+    C.check(C.lib().rtpb_shutdown())
+    after = system.ray_trace(rays, m0, m1)
+    assert np.array_equal(after, before, equal_nan=True)
+    x = torch.from_numpy(rays).to(DEV)
+    assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), before, equal_nan=True)
