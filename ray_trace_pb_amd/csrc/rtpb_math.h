@@ -119,7 +119,14 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     const double s2 = __builtin_fma(d0, h1, s1);
     const double d1 = __builtin_fma(-s2, s2, v);
     double s3 = __builtin_fma(d1, h1, s2);
+#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same set with three float64 compares
     const bool slow = (v >= 0.0 && v < 0x1p-767) || v == __builtin_inf();
+#else
+    // the same set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
+    // compare of the high word (negative values and NaN have it at or above 0x10000000 unsigned)
+    const bool slow = __builtin_amdgcn_class(v, 0x2E0) ||
+                      static_cast<uint32_t>(__double2hiint(v)) < 0x10000000u;
+#endif
     if constexpr (G::kDefer) {
         // +-0 and +inf (normal incidence gives sqrt(0) on every axial ray) are their own square roots:
         // a select, so only 0 < v < 2^-767 is left to the re-trace
@@ -195,8 +202,15 @@ __device__ __forceinline__ bool fastdiv_den_ok(double b) {
     return (m >= 0x1p-120 && m <= 0x1p120) || __builtin_amdgcn_class(b, 0x267);   // 0x267: +-0, +-inf, NaN
 }
 __device__ __forceinline__ bool fastdiv_num_ok(double a) {
+#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same test with two float64 compares
     const double m = __builtin_fabs(a);
     return (m >= 0x1p-800 && m <= 0x1p600) || __builtin_amdgcn_class(a, 0x267);
+#else
+    // biased exponent in [223, 1622], i.e. 2^-800 <= |a| < 2^600 (a subset of the exact range), on the
+    // high word with 32-bit integer ops: (hi << 1) drops the sign, the subtraction wraps below 223
+    const uint32_t h2 = static_cast<uint32_t>(__double2hiint(a)) << 1;
+    return h2 - (223u << 21) < (1400u << 21) || __builtin_amdgcn_class(a, 0x267);
+#endif
 }
 __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
     const double q0 = a * y;
