@@ -198,8 +198,14 @@ struct Rcp {
 
 #if defined(RTPB_FASTDIV)
 __device__ __forceinline__ bool fastdiv_den_ok(double b) {
+#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same test with two float64 compares
     const double m = __builtin_fabs(b);
     return (m >= 0x1p-120 && m <= 0x1p120) || __builtin_amdgcn_class(b, 0x267);   // 0x267: +-0, +-inf, NaN
+#else
+    // biased exponent in [903, 1142]: 2^-120 <= |b| < 2^120 (see fastdiv_num_ok); 0x267: +-0, +-inf, NaN
+    const uint32_t h2 = static_cast<uint32_t>(__double2hiint(b)) << 1;
+    return h2 - (903u << 21) < (240u << 21) || __builtin_amdgcn_class(b, 0x267);
+#endif
 }
 __device__ __forceinline__ bool fastdiv_num_ok(double a) {
 #if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same test with two float64 compares
