@@ -197,6 +197,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             // both planes of the surface share one LDS round trip
             if (st_after) tile_write<TS>(tile_b, lane, after);
             if (st_at || st_after) lds_wait();
+#if defined(RTPB_EXP_FLUSH_SYNC)            // experiment only: the workgroup's waves flush each plane together
+            if constexpr (kB > 64) __syncthreads();
+#endif
             if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
             if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
         } else if (valid) {
