@@ -275,7 +275,13 @@ template <typename TS, bool NT>
 __device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
                                            int64_t n, int lane) {
     constexpr int kRec = 8 * sizeof(TS);
-    constexpr int kAux = NT ? 2 : 0;                     // gfx950 cache policy: nt
+#if defined(RTPB_EXP_STORE_AUX)              // experiment only: other cache-policy bits (1 sc0, 2 nt, 16 sc1)
+    constexpr int kAux = NT ? RTPB_EXP_STORE_AUX : 0;
+#else
+    // gfx950 cache policy nt + sc1 (streaming, system scope): 0.5 % faster than nt alone on C2-C4 in
+    // interleaved A/B (profiles/r02/experiments/ab_aux*.log); without nt the C3 history is 26 % slower
+    constexpr int kAux = NT ? (2 | 16) : 0;
+#endif
     const int64_t left = n - ray0;
     const int nbytes = static_cast<int>((left < 64 ? left : 64) * kRec);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
