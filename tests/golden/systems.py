@@ -416,7 +416,7 @@ def lightsheet(rt, mat, rad_curv, nrays=1001):
 
 # ------------------------------------------------------------------ randomised systems (fuzz)
 FUZZ_GLASSES = ("Bk7", "Sf10", "Sf2", "Nsf11", "Nbaf10", "FusedSilica", "Nlak22", "Nsf6ht", "Nsk11")
-N_FUZZ = 16
+N_FUZZ = 32
 
 
 def _tilted(rng, axis, p, scale):
