@@ -229,15 +229,6 @@ constexpr int kTileBytes = 64 * 64;    // 64 records of <= 64 B
 typedef double v2d __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void gstore(double2* p, const double2& v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
-    else *p = v;
-}
-__device__ __forceinline__ void gstore(float4* p, const float4& v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
-    else *p = v;
-}
-
 // Stage one record into the wave's tile (XOR-swizzled slots)
 template <typename TS>
 __device__ __forceinline__ void tile_write(uint4* __restrict__ tile, int lane, const Ray<double>& r) {
