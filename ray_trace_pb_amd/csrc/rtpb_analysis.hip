@@ -121,17 +121,20 @@ struct SweepArgs {
 template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
 
-// Two rays per lane: block b covers tiles 2b and 2b+1 of its group; both rays go through each surface
-// in one straight-line region (propagate_surface_pair) so two independent dependency chains
-// interleave (-6 % vs one ray per lane); each tile is reduced separately, with the same tree as
+// kSweepRays rays per lane: block b covers tiles kSweepRays*b ... of its group; the rays go through each
+// surface in one straight-line region (propagate_surface_multi) so independent dependency chains
+// interleave (two: -6 % vs one ray per lane); each tile is reduced separately, with the same tree as
 // spot_partial_kernel.
+#ifndef RTPB_SWEEP_RPL
+#define RTPB_SWEEP_RPL 2
+#endif
+constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per block)
+
 template <typename TS, int FEAT>
 __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     __shared__ double red[kStats][kBlock];
     const int64_t g = blockIdx.y;
-    const int64_t tileA = 2 * int64_t(blockIdx.x), tileB = tileA + 1;
-    const int64_t jA = tileA * kBlock + threadIdx.x, jB = tileB * kBlock + threadIdx.x;
-    const bool okA = jA < a.gsize, okB = jB < a.gsize;
+    const int64_t tile0 = kSweepRays * int64_t(blockIdx.x);
     const double* gp = a.grp + 4 * g;
     auto gen = [&](int64_t j) {
         const int64_t jj = j < a.gsize ? j : 0;
@@ -147,11 +150,13 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
         r.wl = stored<TS>(gp[3]);
         return r;
     };
-    Ray<double> rA = gen(jA), rB = gen(jB);
+    Ray<double> r[kSweepRays];
+#pragma unroll
+    for (int q = 0; q < kSweepRays; ++q) r[q] = gen((tile0 + q) * kBlock + threadIdx.x);
     const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
     const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
     const cptr<double> table = (cptr<double>)(a.table);
-    const double wl0 = rA.wl;                          // one wavelength per group
+    const double wl0 = r[0].wl;                        // one wavelength per group
     const Rcp<double> iwl = make_rcp(wl0);             // shared divisor of every phase update
     // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the
     // kernel's own material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
@@ -164,10 +169,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     for (int s = 0; s < a.nsurf; ++s) {
         const double n_next = mat_n(s + 1);
         const DevSurface<double> sd = load_surface<double>(surf + s);
-        Ray<double> aA, aB;
-        propagate_surface_pair<double, (FEAT & 1) != 0>(sd, rA, rB, n_cur, n_next, iwl, iwl, aA, aB);
-        rA = aA;
-        rB = aB;
+        propagate_surface_multi<double, (FEAT & 1) != 0, kSweepRays>(sd, r, n_cur, n_next, iwl);
         n_cur = n_next;
     }
     auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
@@ -189,8 +191,11 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
             a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
         __syncthreads();
     };
-    reduce(rA, okA, tileA);
-    reduce(rB, okB, tileB);
+#pragma unroll
+    for (int q = 0; q < kSweepRays; ++q) {
+        const int64_t tile = tile0 + q;
+        reduce(r[q], tile * kBlock + threadIdx.x < a.gsize, tile);
+    }
 }
 
 // griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
@@ -354,7 +359,7 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
     }
     a.nsurf = plan->nsurf;
-    const dim3 grid(static_cast<unsigned>((tiles + 1) / 2), static_cast<unsigned>(n_groups));
+    const dim3 grid(static_cast<unsigned>((tiles + kSweepRays - 1) / kSweepRays), static_cast<unsigned>(n_groups));
     auto go = [&](auto tag) {
         using TS = decltype(tag);
         const int f = plan->feat & 3;                 // lens / POLY6 code; tables are always compiled in here

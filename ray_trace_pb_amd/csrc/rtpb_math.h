@@ -632,6 +632,37 @@ RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, co
     }
 }
 
+// R independent rays through the same surface, in place (R = 2 is propagate_surface_pair).
+template <typename T, bool WITH_LENS, int R, class G = GuardBranch>
+RTPB_HD void propagate_surface_multi(const DevSurface<T>& s, Ray<T> (&r)[R], T n1, T n2, const Rcp<T>& iwl,
+                                     G* g = nullptr) {
+    if constexpr (R == 2) {
+        Ray<T> a, b;
+        propagate_surface_pair<T, WITH_LENS>(s, r[0], r[1], n1, n2, iwl, iwl, a, b, g);
+        r[0] = a;
+        r[1] = b;
+    } else {
+        auto none = [](const Ray<T>&) {};
+        Ray<T> o[R];
+        const int kind = s.kind;
+        if (WITH_LENS && kind == PERFECT_LENS) {
+#pragma unroll
+            for (int q = 0; q < R; ++q) surface_step<T, PERFECT_LENS>(s, r[q], n1, n2, iwl, none, o[q], g);
+        } else if (kind == SPHERE) {
+#pragma unroll
+            for (int q = 0; q < R; ++q) surface_step<T, SPHERE>(s, r[q], n1, n2, iwl, none, o[q], g);
+        } else if (kind == PLANE_MIRROR) {
+#pragma unroll
+            for (int q = 0; q < R; ++q) surface_step<T, PLANE_MIRROR>(s, r[q], n1, n2, iwl, none, o[q], g);
+        } else {
+#pragma unroll
+            for (int q = 0; q < R; ++q) surface_step<T, FLAT>(s, r[q], n1, n2, iwl, none, o[q], g);
+        }
+#pragma unroll
+        for (int q = 0; q < R; ++q) r[q] = o[q];
+    }
+}
+
 template <typename T, bool WITH_LENS = true>
 RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
     propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, make_rcp(r.wl), [&](const Ray<T>& v) { at = v; }, after);
