@@ -149,6 +149,27 @@ class Workload:
         return self.out.numel() * self.out.element_size() / (f0.elapsed_time(f1) / 5 * 1e-3) / 1e9
 
 
+def stream_copy_rate(device, nbytes=4 << 30, reps=10):
+    """Measured copy rate of the device (GB/s, read + write bytes of a torch copy_ between two fresh
+    `nbytes` buffers): the measured stream-copy figure SURVEY §8(d) asks for beside the 8 TB/s spec.  It is
+    torch's elementwise copy kernel, not a tuned one (4.7 TB/s on MI355X, below the trace kernel's own
+    rate), so `frac` stays priced against the spec peak."""
+    import torch
+    src = torch.ones(nbytes // 8, dtype=torch.float64, device=device)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    rate = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return rate
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -267,7 +288,7 @@ def measure_traffic(args, config):
     return (2.0 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0, None
 
 
-def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None):
+def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None, copy=None):
     achieved = wl.alg_bytes / (kernel_ms * 1e-3) / 1e9
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
          "traffic": traffic, "kernel": "trace_kernel", "kernel_ms_avg": kernel_ms,
@@ -276,6 +297,8 @@ def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None):
          "alg_bytes_per_ray_surface": wl.bytes_per_ray / wl.S}
     if fill:
         r.update(output_fill_GBps=fill, frac_of_output_fill=achieved / fill)
+    if copy:
+        r.update(torch_copy_GBps=copy, frac_of_torch_copy=achieved / copy)
     if traffic_note:
         r["traffic_note"] = traffic_note
     return r
@@ -315,6 +338,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     fill = wl.fill_rate() if rank == 0 else None
+    copy = stream_copy_rate(dev) if rank == 0 else None
 
     per_rank = None
     if world > 1:
@@ -336,7 +360,7 @@ def main():
         traffic, note = (None, None)
         if world == 1 and args.traffic == "auto":
             traffic, note = measure_traffic(args, args.config)
-        rl = roofline(wl, kernel_ms_max, traffic, note, fill)
+        rl = roofline(wl, kernel_ms_max, traffic, note, fill, copy)
         rl["kernel_ms_max_rank"] = kernel_ms_max
         line = {
             "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
@@ -363,7 +387,7 @@ def main():
             line["secondary"] = {"config": "BASELINE configs[1]: " + w2.workload, "dtype": "f64",
                                  "value": w2.n * w2.S * max(args.steps, 50) / e2, "unit": UNIT,
                                  "rays": w2.n, "surfaces": w2.S,
-                                 "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate())}
+                                 "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate(), copy)}
         if world == 1 and args.cpu_baseline == "auto":
             cpu = cpu_time(args.config, 8.0)
             cpu["cpu_model"] = cpu_model()
