@@ -130,8 +130,15 @@ __device__ __forceinline__ double stored(double v) { return static_cast<double>(
 #endif
 constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per block)
 
+// Occupancy: held to >= 7 waves per SIMD (<= 72 VGPRs; the compiler spills 6-8 values to scratch outside
+// the surface loop) -- 2.4 % faster than its natural 83 VGPRs / 5 waves on the full C5 sweep, 6 and 8 waves
+// in between (experiments/ab_sweep_wpe*.log, bit-identical).  RTPB_SWEEP_WPE overrides it (A/B builds).
+#ifndef RTPB_SWEEP_WPE
+#define RTPB_SWEEP_WPE 7
+#endif
+#define RTPB_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(RTPB_SWEEP_WPE, 8)))
 template <typename TS, int FEAT>
-__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs a) {
     __shared__ double red[kStats][kBlock];
     const int64_t g = blockIdx.y;
     const int64_t tile0 = kSweepRays * int64_t(blockIdx.x);

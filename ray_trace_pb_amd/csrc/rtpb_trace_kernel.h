@@ -255,7 +255,10 @@ hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
     // waves per SIMD (<= 80 VGPRs, no spill); everything else keeps the compiler's choice (the history
     // kernels are bound by their LDS tiles and store stream: 6-8 waves measured no faster; the float32
     // final-only variants would spill)
-#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? 6 : 1)
+#ifndef RTPB_FINAL_WPE
+#define RTPB_FINAL_WPE 6
+#endif
+#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? RTPB_FINAL_WPE : 1)
 #endif
     switch (feat) {
     case 0: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(0), 0>(a, st);
