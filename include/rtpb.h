@@ -274,8 +274,6 @@ int rtpb_distinct_keys(int32_t device, const void* col, int32_t dtype, int64_t n
    streamed out and never re-read by the kernel); 0 = default cache policy.
    "stage_input": 1 = also load AOS input records through the LDS tile (1 KiB per load instruction);
    0 (default) = 4 x 16-byte loads per lane.
-   "waves_per_eu": 0 (default: compiler choice, 4 waves/SIMD) or 5 = occupancy target for the
-   AOS->AOS staged kernel (the compiler then spills to scratch to fit).
    "host_chunk_mib": input + output bytes per pipelined chunk of rtpb_trace_host (default 128).
    "indexed_materials": 1 (default) = plans created from now on whose TABLE materials all share one
    key set (and that have no POLY6 material) also tabulate every other material at those keys, so the

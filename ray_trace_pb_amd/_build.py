@@ -20,15 +20,17 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
          "-I", os.path.join(ROOT, "include")]
 
 
-def sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+def sources(csrc=CSRC):
+    return sorted(glob.glob(os.path.join(csrc, "*.hip")))
 
 
-def build(force=False, verbose=True, extra_flags=(), out=None):
+def build(force=False, verbose=True, extra_flags=(), out=None, csrc=CSRC):
+    """Compile csrc/*.hip and link them into `out`.  `csrc` / `extra_flags` let tools build experiment
+    variants from a patched copy of the sources (tools/exp_build.py); the product build uses neither."""
     out = out or OUT
-    srcs = sources()
-    deps = srcs + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "rtpb.h")]
-    if not force and not extra_flags and os.path.exists(out) and \
+    srcs = sources(csrc)
+    deps = srcs + glob.glob(os.path.join(csrc, "*.h")) + [os.path.join(ROOT, "include", "rtpb.h")]
+    if not force and not extra_flags and csrc == CSRC and os.path.exists(out) and \
             all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     os.makedirs(OBJ, exist_ok=True)

@@ -33,11 +33,7 @@ constexpr int kBlock = 256;               // auxiliary kernels
 // The trace kernel runs one wave per workgroup: a workgroup's LDS tile and wave slot are released the
 // moment its wave finishes, so the dispatcher refills CUs wave by wave instead of waiting for the
 // slowest of four (-6 % kernel time on C2 f64 full history vs 256-thread workgroups, same occupancy).
-#if defined(RTPB_EXP_TRACE_BLOCK)          // experiment builds only (tools/ab_libs.py)
-constexpr int kTraceBlock = RTPB_EXP_TRACE_BLOCK;
-#else
 constexpr int kTraceBlock = 64;
-#endif
 constexpr int kMaxDevices = 64;
 
 // Thread-local message of the last failure (rtpb_last_error) and the helper every entry point uses.
@@ -96,7 +92,7 @@ extern template hipError_t launch_trace<float, float>(const TraceArgs<float, flo
 extern template hipError_t launch_trace<double, float>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
 extern template hipError_t launch_trace<float, double>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
 // tuning knobs (rtpb_set_tuning, defined in rtpb_trace.hip)
-extern std::atomic<int> g_aos_staging, g_nt_stores, g_waves_per_eu, g_stage_input, g_host_chunk_mib, g_indexed_materials;
+extern std::atomic<int> g_aos_staging, g_nt_stores, g_stage_input, g_host_chunk_mib, g_indexed_materials;
 
 // Descriptors are read-only for the whole launch: read them through the constant address space so
 // the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.
@@ -266,13 +262,9 @@ template <typename TS, bool NT>
 __device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* __restrict__ plane, int64_t ray0,
                                            int64_t n, int lane) {
     constexpr int kRec = 8 * sizeof(TS);
-#if defined(RTPB_EXP_STORE_AUX)              // experiment only: other cache-policy bits (1 sc0, 2 nt, 16 sc1)
-    constexpr int kAux = NT ? RTPB_EXP_STORE_AUX : 0;
-#else
     // gfx950 cache policy nt + sc1 (streaming, system scope): 0.5 % faster than nt alone on C2-C4 in
     // interleaved A/B (profiles/r02/experiments/ab_aux*.log); without nt the C3 history is 26 % slower
     constexpr int kAux = NT ? (2 | 16) : 0;
-#endif
     const int64_t left = n - ray0;
     const int nbytes = static_cast<int>((left < 64 ? left : 64) * kRec);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(

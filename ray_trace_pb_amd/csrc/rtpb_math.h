@@ -78,12 +78,10 @@ template <> RTPB_HD float qnan<float>() { return __builtin_nanf(""); }
 template <typename T> RTPB_HD bool is_nan(T v) { return v != v; }
 
 // Device fast paths of the f64 division and square root that are bit-identical to the compiler's own
-// expansions (see "shared-divisor quotients" below and tsqrt); -DRTPB_NO_FASTDIV / -DRTPB_NO_FASTSQRT
-// build without them (A/B experiments).
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTDIV)
+// expansions (see "shared-divisor quotients" below and tsqrt); host builds (the CPU harness) use the
+// plain operators.
+#if defined(__HIP_DEVICE_COMPILE__)
 #define RTPB_FASTDIV 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTPB_NO_FASTSQRT)
 #define RTPB_FASTSQRT 1
 #endif
 
@@ -119,23 +117,17 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     const double s2 = __builtin_fma(d0, h1, s1);
     const double d1 = __builtin_fma(-s2, s2, v);
     double s3 = __builtin_fma(d1, h1, s2);
-#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same set with three float64 compares
-    const bool slow = (v >= 0.0 && v < 0x1p-767) || v == __builtin_inf();
-#else
-    // the same set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
+    // the set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
     // compare of the high word (negative values and NaN have it at or above 0x10000000 unsigned)
     const bool slow = __builtin_amdgcn_class(v, 0x2E0) ||
                       static_cast<uint32_t>(__double2hiint(v)) < 0x10000000u;
-#endif
     if constexpr (G::kDefer) {
         // +-0 and +inf (normal incidence gives sqrt(0) on every axial ray) are their own square roots:
         // a select, so only 0 < v < 2^-767 is left to the re-trace
         if (v == 0.0 || v == __builtin_inf()) s3 = v;
         g->bad = g->bad || (v > 0.0 && v < 0x1p-767);
     } else {
-#if !defined(RTPB_EXP_NO_GUARDS)           // experiment only: the cost of the range guards (inexact)
         if (__builtin_expect(slow, 0)) s3 = sqrt(v);
-#endif
     }
     return s3;
 #else
@@ -198,25 +190,15 @@ struct Rcp {
 
 #if defined(RTPB_FASTDIV)
 __device__ __forceinline__ bool fastdiv_den_ok(double b) {
-#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same test with two float64 compares
-    const double m = __builtin_fabs(b);
-    return (m >= 0x1p-120 && m <= 0x1p120) || __builtin_amdgcn_class(b, 0x267);   // 0x267: +-0, +-inf, NaN
-#else
     // biased exponent in [903, 1142]: 2^-120 <= |b| < 2^120 (see fastdiv_num_ok); 0x267: +-0, +-inf, NaN
     const uint32_t h2 = static_cast<uint32_t>(__double2hiint(b)) << 1;
     return h2 - (903u << 21) < (240u << 21) || __builtin_amdgcn_class(b, 0x267);
-#endif
 }
 __device__ __forceinline__ bool fastdiv_num_ok(double a) {
-#if defined(RTPB_FLOAT_RANGE_CHECKS)      // A/B only: the same test with two float64 compares
-    const double m = __builtin_fabs(a);
-    return (m >= 0x1p-800 && m <= 0x1p600) || __builtin_amdgcn_class(a, 0x267);
-#else
     // biased exponent in [223, 1622], i.e. 2^-800 <= |a| < 2^600 (a subset of the exact range), on the
     // high word with 32-bit integer ops: (hi << 1) drops the sign, the subtraction wraps below 223
     const uint32_t h2 = static_cast<uint32_t>(__double2hiint(a)) << 1;
     return h2 - (223u << 21) < (1400u << 21) || __builtin_amdgcn_class(a, 0x267);
-#endif
 }
 __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
     const double q0 = a * y;
@@ -262,9 +244,7 @@ RTPB_HD T div1(T a, const Rcp<T>& r, G* g = nullptr) {
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
-#if !defined(RTPB_EXP_NO_GUARDS)
             if (__builtin_expect(slow, 0)) q = a / r.b;
-#endif
         }
         return q;
     }
@@ -284,9 +264,7 @@ RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
-#if !defined(RTPB_EXP_NO_GUARDS)
             if (__builtin_expect(slow, 0)) q = a / b;
-#endif
         }
         return q;
     }
@@ -305,12 +283,10 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
-#if !defined(RTPB_EXP_NO_GUARDS)
             if (__builtin_expect(slow, 0)) {
                 x = x / r.b; y = y / r.b; z = z / r.b;
                 return;
             }
-#endif
         }
         x = qx; y = qy; z = qz;
         return;
@@ -326,9 +302,6 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 // materials (rtpb_plan::feat).
 template <typename T, bool WITH_POLY6 = true, bool WITH_TABLE = true, typename TablePtr, class G = GuardBranch>
 RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table, G* g = nullptr) {
-#if defined(RTPB_EXP_NO_MATERIAL)          // experiment only: material evaluation cost (wrong indices)
-    return T(1) + m.c[0] * T(1e-3) + wl * T(1e-9);
-#endif
     switch (m.kind) {
     case CONSTANT:
         return m.c[0];                                               // MAT:72-79
@@ -503,9 +476,6 @@ RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
 // FlatSurface / PlaneMirror .is_pt_on_surface (RT:1339-1347, RT:1405-1412)
 template <typename T>
 RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
-#if defined(RTPB_EXP_NO_ONSURFACE)       // experiment only
-    return p.x == p.x;
-#endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
     const T h = rx * s.nrm[0] + ry * s.nrm[1] + rz * s.nrm[2];
     return tabs<T>(h) < s.tol && rx * rx + ry * ry + rz * rz <= s.ap_sq;      // norm(p - c) <= aperture
@@ -514,9 +484,6 @@ RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
 // SphericalSurface.is_pt_on_surface (RT:1518-1535): aperture about the ORIGIN-through input axis
 template <typename T>
 RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
-#if defined(RTPB_EXP_NO_ONSURFACE)       // experiment only
-    return p.x == p.x;
-#endif
     const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
     const T d2 = rx * rx + ry * ry + rz * rz;
     const bool on = d2 >= s.shell_lo && d2 <= s.shell_hi;                      // |norm(p - c) - |R|| < tol

@@ -11,7 +11,6 @@ namespace rtpbi {
 // tuning knobs (rtpb_set_tuning); process-wide, read by launch_trace
 std::atomic<int> g_aos_staging{1};
 std::atomic<int> g_nt_stores{1};
-std::atomic<int> g_waves_per_eu{0};
 std::atomic<int> g_stage_input{0};
 std::atomic<int> g_host_chunk_mib{128};
 std::atomic<int> g_indexed_materials{1};          // read at plan creation (rtpb_plan_create)
@@ -342,11 +341,6 @@ int rtpb_set_tuning(const char* key, int64_t value) {
     }
     if (std::strcmp(key, "indexed_materials") == 0) {
         g_indexed_materials.store(value != 0);
-        return RTPB_OK;
-    }
-    if (std::strcmp(key, "waves_per_eu") == 0) {
-        if (value != 0 && value != 5) return fail(RTPB_E_INVALID, "waves_per_eu must be 0 or 5");
-        g_waves_per_eu.store(static_cast<int>(value));
         return RTPB_OK;
     }
     return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);

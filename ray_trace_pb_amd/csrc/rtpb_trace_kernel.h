@@ -50,13 +50,8 @@ constexpr int trace_block(int out_layout, int store) {
 // without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
 // table lookup the surface loop never waits on the vmcnt counter, which on gfx950 would also wait for
 // every history store in flight (see kLdsTablePairs).  rtpb_plan::feat picks the variant.
-#if defined(RTPB_EXP_MAXW)                  // experiment only: cap the waves per SIMD of the history kernels
-#define RTPB_MAXW(ST) (((ST) & 8) ? 8 : RTPB_EXP_MAXW)
-#else
-#define RTPB_MAXW(ST) 8
-#endif
 template <typename TIN, typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
-__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, RTPB_MAXW(STORE))))
+__global__ __launch_bounds__(trace_block(OUT_LAYOUT, STORE)) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 void trace_kernel(TraceArgs<TIN, TS> a) {
     constexpr int kB = trace_block(OUT_LAYOUT, STORE);
     using T = double;
@@ -80,44 +75,20 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     // 10 f32 waves per SIMD in the all-planes mode, so registers set the f32 occupancy)
     __shared__ uint4 tiles[kB / 64][kFinal ? 1 : 2][kTileBytes / 16 * sizeof(TS) / 8];
     const int lane = threadIdx.x & 63;
-    // one block of kB rays (the whole kernel, or one step of the persistent experiment's loop)
+    // one block of kB rays per workgroup (blocks go round-robin over the XCDs: measured faster than
+    // XCD-contiguous block ranges).  The body is a lambda of the block index; called once.
     auto body = [&](const int64_t blk) {
-#if defined(RTPB_EXP_XCD_REMAP)             // experiment only: each XCD takes a contiguous range of ray blocks
-    // workgroups are dispatched round-robin over the 8 XCDs: block b runs on XCD b % 8
-    const uint32_t nb = gridDim.x, per = nb / 8, xcd = blockIdx.x % 8, k = blockIdx.x / 8;
-    const uint32_t bid = blockIdx.x < per * 8 ? xcd * per + k : blockIdx.x;
-    const int64_t i = static_cast<int64_t>(bid) * kB + threadIdx.x;
-#elif defined(RTPB_EXP_SCATTER)           // experiment only: ray blocks visited in a scattered order
-    // block b -> (b * RTPB_EXP_SCATTER) mod nb, a bijection when nb is not a multiple of the prime
-    const int64_t nb = gridDim.x;
-    const int64_t bs = (nb % RTPB_EXP_SCATTER) ? (blk * RTPB_EXP_SCATTER) % nb : blk;
-    const int64_t i = bs * kB + threadIdx.x;
-#else
     const int64_t i = blk * kB + threadIdx.x;
-#endif
     const int64_t ray0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(i - lane)));  // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
-#if defined(RTPB_EXP_STAGGER)              // experiment only: desynchronise the first round of waves
-    // consecutive workgroups go to different XCDs, so the delay step uses blockIdx / 8 (varies inside
-    // an XCD); 0..7 steps of s_sleep(RTPB_EXP_STAGGER) (64 cycles per unit)
-    if (blockIdx.x < 8192)
-        for (unsigned k = 0; k < ((blockIdx.x >> 3) & 7u); ++k) __builtin_amdgcn_s_sleep(RTPB_EXP_STAGGER);
-#endif
     const bool valid = i < a.n;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
     uint4* tile_b = tiles[threadIdx.x >> 6][kFinal ? 0 : 1];
     Ray<T> r;
-#if defined(RTPB_EXP_NO_INPUT)             // experiment only: no input reads (write-only memory path)
-    {
-        const T v = T(i);
-        r.x = v; r.y = v; r.z = v; r.dx = v; r.dy = v; r.dz = v; r.ph = v; r.wl = T(0.5);
-    }
-#else
     // staged input loads use the output tile, so they need the input records to be TS-sized
     if constexpr (kStaged && IN_LAYOUT == RTPB_AOS && (STORE & 4) && std::is_same<TIN, TS>::value)
         r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
     else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
-#endif
     const T wl0 = r.wl;
     const Rcp<T> iwl = make_rcp(wl0);                    // shared divisor of every phase update
     TS* __restrict__ out = a.out;
@@ -186,20 +157,11 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             }
         };
         Ray<T> after;
-#if defined(RTPB_EXP_NO_COMPUTE)           // experiment only: the kernel's pure memory path
-        after = r;
-        after.ph = r.ph + n_next + n_cur;
-        emit_at(r);
-#else
         propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
-#endif
         if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
             if (st_after) tile_write<TS>(tile_b, lane, after);
             if (st_at || st_after) lds_wait();
-#if defined(RTPB_EXP_FLUSH_SYNC)            // experiment only: the workgroup's waves flush each plane together
-            if constexpr (kB > 64) __syncthreads();
-#endif
             if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
             if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
         } else if (valid) {
@@ -209,11 +171,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         n_cur = n_next;
     }
     };
-#if defined(RTPB_EXP_PERSIST)              // experiment only: persistent grid, block-stride loop
-    for (int64_t blk = blockIdx.x; blk * kB < a.n; blk += gridDim.x) body(blk);
-#else
     body(static_cast<int64_t>(blockIdx.x));
-#endif
 }
 
 
@@ -224,42 +182,18 @@ hipError_t launch_w(const TraceArgs<TI, T>& a, hipStream_t st) {
     const int64_t blocks = (a.n + kB - 1) / kB;
     const size_t lds = (FEAT & 16)        ? static_cast<size_t>(a.nkeys) * (a.nsurf + 2) * sizeof(double)
                        : (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
-#if defined(RTPB_EXP_PERSIST)
-    static int resident = 0;                     // experiment: one wave slot per workgroup of the grid
-    if (!resident) {
-        int per_cu = 0, dev = 0, cus = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_kernel<TI, T, IL, OL, ST, W, FEAT>, kB, lds);
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        resident = per_cu * cus * RTPB_EXP_PERSIST;
-    }
-    const int64_t grid = blocks < resident ? blocks : resident;
-#else
-    const int64_t grid = blocks;
-#endif
-    hipLaunchKernelGGL((trace_kernel<TI, T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(grid)), dim3(kB), lds,
+    hipLaunchKernelGGL((trace_kernel<TI, T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), lds,
                        st, a);
     return hipGetLastError();
 }
 
 template <typename TI, typename T, int IL, int OL, int ST>
 hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
-    if constexpr (IL == RTPB_AOS && OL == RTPB_AOS && ST == 3) {       // occupancy experiments (tuning)
-        const int w = g_waves_per_eu.load();
-        if (w == 5) return launch_w<TI, T, IL, OL, ST, 5, 15>(a, st);
-    }
-#if defined(RTPB_EXP_WPE)                  // experiment only: minimum waves per SIMD for every variant
-#define RTPB_WPE(F) RTPB_EXP_WPE
-#else
     // float64 final-plane-only kernels (compute-bound: the C5 / focus-finding mode) are held to >= 6
-    // waves per SIMD (<= 80 VGPRs, no spill); everything else keeps the compiler's choice (the history
-    // kernels are bound by their LDS tiles and store stream: 6-8 waves measured no faster; the float32
-    // final-only variants would spill)
-#ifndef RTPB_FINAL_WPE
-#define RTPB_FINAL_WPE 6
-#endif
-#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? RTPB_FINAL_WPE : 1)
-#endif
+    // waves per SIMD (<= 80 VGPRs, no spill; 7 and 8 measured slower); everything else keeps the
+    // compiler's choice (the history kernels are bound by their LDS tiles and store stream: 6-8 waves
+    // measured no faster; the float32 final-only variants would spill)
+#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? 6 : 1)
     switch (feat) {
     case 0: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(0), 0>(a, st);
     case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
@@ -279,8 +213,7 @@ hipError_t launch_trace(const TraceArgs<TI, T>& a, int il, int ol, int feat, hip
     const int last = 2 * a.nsurf;                       // planes='final': only the last plane stored
     const bool final_only = a.nsurf > 0 && (last < 64 ? (a.mask_lo == (1ull << last) && a.mask_hi == 0)
                                                       : (a.mask_lo == 0 && a.mask_hi == (1ull << (last - 64))));
-    if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load() &&
-        g_waves_per_eu.load() == 0)
+    if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load())
         return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 11>(a, feat, st);
     if constexpr (!std::is_same<TI, T>::value) {
         // input and storage types differ: AOS input only (rtpb_trace checks), no staged-input variant

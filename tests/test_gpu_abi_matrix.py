@@ -80,8 +80,8 @@ def _trace(plan, x, in_code, in_layout, in_stride, n, nslots, out_code, out_layo
     return np.stack(slots) if slots else np.zeros((0, n, 8), NP_DT[out_code]), pad_ok
 
 
-KNOBS = [None, ("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1), ("waves_per_eu", 5), ("indexed_materials", 0)]
-KNOB_DEFAULT = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0, "indexed_materials": 1}
+KNOBS = [None, ("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1), ("indexed_materials", 0)]
+KNOB_DEFAULT = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "indexed_materials": 1}
 
 
 @pytest.fixture(params=KNOBS, ids=lambda k: "default" if k is None else "%s=%d" % k)

@@ -117,12 +117,12 @@ def test_soa_layout_matches_aos():
     assert np.array_equal(soa.transpose(1, 2).cpu().numpy(), ref, equal_nan=True)
 
 
-@pytest.mark.parametrize("knob", [("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1), ("waves_per_eu", 5)])
+@pytest.mark.parametrize("knob", [("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1)])
 def test_tuning_variants_bitwise(knob):
     """Every store/load strategy is a pure data-movement change: bit-identical histories."""
     system, m0, m1, rays, ref = build_case("stress")
     lib = C.lib()
-    default = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0}[knob[0]]
+    default = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0}[knob[0]]
     C.check(lib.rtpb_set_tuning(knob[0].encode(), knob[1]))
     try:
         r32 = rays.astype(np.float32)

@@ -1,8 +1,7 @@
 """A/B several builds of librtpb.so in ONE process (interleaved, randomised order, median of rounds).
 
 Each extra library is an experiment build of the same sources, e.g.
-    python -c "from ray_trace_pb_amd import _build; _build.build(extra_flags=['-DRTPB_EXP_NO_ONSURFACE'],
-               out='ray_trace_pb_amd/exp_noons.so')"
+    python tools/exp_build.py --out ray_trace_pb_amd/exp_noons.so -DRTPB_EXP_NO_ONSURFACE
 (`-DRTPB_EXP_NO_ONSURFACE` drops work and is NOT bit-exact) -- used only to find where kernel time goes,
 never shipped.
 

@@ -2,8 +2,7 @@
 
 A variant is (library build, tuning knobs): the in-tree librtpb.so with its knobs (e.g. rays_per_lane=2)
 and optional experiment builds of other sources or flags, e.g.
-    python -c "from ray_trace_pb_amd import _build; _build.build(extra_flags=['-DRTPB_EXP_NO_COMPUTE'],
-               out='ray_trace_pb_amd/exp_nocomp.so')"
+    python tools/exp_build.py --out ray_trace_pb_amd/exp_nocomp.so -DRTPB_EXP_NO_COMPUTE
 (experiment builds may drop work -- they are never shipped).  Every variant's history is compared with the
 first variant's (bit for bit, NaN pattern included) unless its library is marked inexact (name contains
 "exp_nocomp").

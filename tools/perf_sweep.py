@@ -72,7 +72,6 @@ def main():
             name, low, x, sel, lc, out, nbytes, units, staged = variants[vi]
             C.check(lib.rtpb_set_tuning(b"aos_staging", staged & 1))
             C.check(lib.rtpb_set_tuning(b"nt_stores", (staged >> 1) & 1))
-            C.check(lib.rtpb_set_tuning(b"waves_per_eu", (staged >> 2) & 15))
             C.check(lib.rtpb_set_tuning(b"stage_input", staged >> 6))
             E.trace_device(low, x, sel, layout_out=lc, out=out)
             torch.cuda.synchronize()
@@ -93,7 +92,6 @@ def main():
         times["copy_768MB"].append(e0.elapsed_time(e1) / args.reps)
     C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
     C.check(lib.rtpb_set_tuning(b"nt_stores", 1))
-    C.check(lib.rtpb_set_tuning(b"waves_per_eu", 0))
     C.check(lib.rtpb_set_tuning(b"stage_input", 0))
     for name, low, x, sel, lc, out, nbytes, units, staged in variants:
         ms = float(np.median(times[name]))

@@ -93,7 +93,7 @@ def main():
             knob, val = t.split("=")
             libs[f"base+{t}"] = libs["base"]
             tun[f"base+{t}"] = (knob.encode(), int(val))
-        defaults = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0, "waves_per_eu": 0}
+        defaults = {"aos_staging": 1, "nt_stores": 1, "stage_input": 0}
         items = [(ln, b) for ln in libs for b in range(len(outs))]
         times = {it: [] for it in items}
         for _ in range(args.rounds):
