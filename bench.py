@@ -1,25 +1,32 @@
-"""Benchmark: ray-surface intersections/s of System.ray_trace on MI355X (BASELINE.json metric).
+"""Benchmark: ray-surface intersections/s of the sequential ray trace on MI355X (BASELINE.json metric).
 
 Headline workload (BASELINE.json configs[2], the largest single-GPU config): the 4f
 relay of scripts/2024_08_08_achromat_imaging.py:13-70 -- object flat, two Thorlabs AC508-075-A-ML
 doublets (Ebaf11 / N-SF11), pupil flat, image flat: S = 9 surfaces -- traced with 5 field points
 h in {0, 4, 8, 12, 16} mm x get_ray_fan(h, 1 deg, 3163, 0.635 um, nphis=3162) = 50,007,030 rays per GPU,
 the full drop-in history (2S+1 = 19 planes) stored as float32 (BASELINE precision; arithmetic float64,
-input rays float64 as the generator makes them, so the history is the reference's rounded once).  A step
-= one System.ray_trace of the GPU's bundle, inputs and outputs resident in HBM.  Multi-GPU: one process
-per GPU (torchrun), each traces its own bundle (rays are independent: no data-path collective) -> weak
-scaling; the job time is the max over ranks.
+input rays float64 as the generator makes them, so the history is the reference's rounded once).  A timed
+step = one launch of the fused trace kernel (rtpb_trace through the C ABI: the body of System.ray_trace,
+RT:641-661) on the GPU's bundle, the plan lowered once before the timed region, inputs and outputs
+resident in HBM.  The whole drop-in call System.ray_trace(torch rays, ...) -- lowering, table keys of the
+Ebaf11 crown (MAT:128-144), output allocation, launch -- is timed separately as `e2e_ms`.
+Multi-GPU: one process per GPU (torchrun), each traces its own C3 bundle (rays are independent: no
+data-path collective) -> weak scaling; the job time is the max over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+The same JSON line carries the other BASELINE configs under "configs":
+  configs[1] C2  AC508-100-B achromat, 1M rays, float64 history (rank 0, N=1 only)
+  configs[3] C4  ideal OPM (scripts/2022_01_25_ray_trace_ideal_opm.py:59-92): the 10001 x 10000 fan
+                 (100,010,000 rays, 11 surfaces, 23-plane float32 history) STRONG-scaled over the ranks:
+                 rank r generates and traces phi rows shard_bounds(10000, N)[r] on its own GPU
+  configs[4] C5  spot-diagram sweep (scripts/2021_10_06_ray_trace_system.py:120-145,186): 64 field points
+                 x 7 wavelengths x 10,001,406-ray fans (4.48e9 rays, 14 surfaces, float64, statistics
+                 only) -- the fused sweep kernel; field points split over the ranks (strong scaling)
+and `cpu_baseline` (N=1, rank 0): oracle/rt_refcost.py -- the reference's algorithm and data flow,
+calibrated against the reference in tests/golden/cpu_calibration.json -- timed on this host on a bounded
+sample of C3, plus C1 (BASELINE configs[0], the plano-convex CPU case).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--configs c2,c4,c5 | none]
     torchrun --nproc-per-node N bench.py --gpus N ...
-
-Rank 0 prints ONE JSON line with the metric, a `roofline` object for the trace kernel (algorithmic bytes /
-average launch duration from HIP events on the launch stream around the timed launches; the PMC-measured
-HBM bytes per launch from a separate rocprofv3 child), per-rank kernel times (N>1), a secondary object
-for BASELINE configs[1] (C2: AC508-100-B achromat, 1M rays, float64), and a `cpu_baseline` object:
-oracle/rt_refcost.py (the reference's algorithm and data flow, calibrated against the reference in
-tests/golden/cpu_calibration.json) timed on this host on a bounded sample of the same workload, plus
-C1 (BASELINE configs[0], the plano-convex CPU case) -- N=1 only.
 """
 import argparse
 import json
@@ -37,9 +44,17 @@ import numpy as np  # noqa: E402
 METRIC = "ray-surface intersections/sec at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 UNIT = "ray-surface intersections/s"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F64_VALU_PEAK_TFLOPS = 78.6    # MI355X FP64 vector: 1/2 of the 157.3 TFLOP/s FP32 vector peak (MI355X_MICROARCH.md:41)
 SEED = 20241008
 C3_FAN = (3163, 3162)          # scripts/2024_08_08_achromat_imaging.py fan at 10M rays per field
 C3_CPU_FAN = (448, 447)        # CPU-baseline sample of C3: 5 fields x 200,256 rays
+C4_FAN = (10001, 10000)        # scripts/2022_01_25_ray_trace_ideal_opm.py:59-92
+C5_FAN = (3163, 3162)          # scripts/2021_10_06_ray_trace_system.py:186 (10M rays per group)
+
+
+def _log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def shard_seed(rank):
@@ -51,13 +66,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
-    ap.add_argument("--scale", type=float, default=1.0, help="c3: fraction of the per-axis fan sizes")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4"], help="headline workload")
+    ap.add_argument("--configs", default="c2,c4,c5", help="other BASELINE configs in the same line ('none')")
+    ap.add_argument("--scale", type=float, default=1.0, help="c3 / c4: fraction of the per-axis fan sizes")
     ap.add_argument("--rays", type=int, default=1_000_000, help="c2: rays per GPU")
-    ap.add_argument("--secondary", default="auto", choices=["auto", "off"], help="C2 float64 object (N=1)")
+    ap.add_argument("--c5-fields", type=int, default=64, help="c5: field points (square grid)")
+    ap.add_argument("--c5-steps", type=int, default=2, help="c5: timed sweeps")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
-                    help="measure HBM bytes with separate rocprofv3 --pmc child runs (rank 0, N=1)")
+                    help="measure HBM bytes / FLOPs with separate rocprofv3 --pmc child runs (rank 0, N=1)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -67,9 +84,10 @@ def dist_env():
 
 
 class Workload:
-    """One BASELINE config on one GPU: system, device-resident input rays, output history buffer."""
+    """One history config on one GPU: system, device-resident input rays, output history buffer.
+    C4 takes the rank's shard (phi rows) of the 100M-ray fan; C3 and C2 a whole bundle per GPU."""
 
-    def __init__(self, config, dev, rank, scale=1.0, c2_rays=1_000_000):
+    def __init__(self, config, dev, rank, world=1, scale=1.0, c2_rays=1_000_000):
         import torch
         import ray_trace_pb_amd.materials as mat
         import ray_trace_pb_amd.raytrace as rt
@@ -90,6 +108,23 @@ class Workload:
                              f"get_ray_fan(h, 1 deg, {nt}, 0.635 um, nphis={nph}), full 19-plane history")
             self.storage = "f32 history (float64 input rays, float64 arithmetic)"
             wl_keys = np.array([0.635])
+        elif config == "c4":
+            import ray_trace_pb_amd.raytrace as rtm
+            self.system, self.m0, self.m1 = systems.c4_system(rt, mat), mat.Constant(systems.OPM_N1), mat.Vacuum()
+            nt, nph = int(C4_FAN[0] * scale), int(C4_FAN[1] * scale)
+            p0, p1 = rtm.shard_bounds(nph, world)[rank]
+            self.total_rays = nt * nph
+            self.rays = torch.empty(((p1 - p0) * nt, 8), dtype=torch.float64, device=dev)
+            theta = 30 * np.pi / 180
+            rt.fan_into(self.rays, np.array([1e-3, 1e-3, 1e-3 * np.tan(theta)]), np.arcsin(1.35 / systems.OPM_N1),
+                        nt, systems.OPM_WAVELENGTH, nph, phi_rows=(p0, p1))
+            self.code = C.RTPB_F32
+            self.workload = (f"C4: ideal OPM of scripts/2022_01_25_ray_trace_ideal_opm.py:59-92 (6 PerfectLens + 5 "
+                             f"flats, one tilted 30 deg, S=11), get_ray_fan(asin(1.35/1.4), {nt}, 532e-6, "
+                             f"nphis={nph}) = {nt * nph} rays sharded by phi rows over the ranks, full 23-plane "
+                             f"history")
+            self.storage = "f32 history (float64 input rays, float64 arithmetic)"
+            wl_keys = np.array([systems.OPM_WAVELENGTH])
         else:
             self.system, self.m0, self.m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
             rays_np = systems.c2_rays(c2_rays, seed=shard_seed(rank))
@@ -109,9 +144,13 @@ class Workload:
         self.out = torch.empty((len(self.planes), self.n, 8), dtype=torch.float64 if w == 8 else torch.float32,
                                device=dev)
         self.stream = torch.cuda.current_stream(dev).cuda_stream
-        # algorithmic bytes per launch: read each input record once (float64), write every stored plane once
-        self.bytes_per_ray = 8 * self.rays.element_size() + 8 * w * len(self.planes)
+        # algorithmic bytes per launch, SURVEY.md §8(d) / BASELINE.md: 16 w (S+1) per ray for the full history
+        # (one read of an input record and one write of each of the 2S+1 planes at the storage width w)
+        self.bytes_per_ray = 16 * w * (self.S + 1)
         self.alg_bytes = self.n * self.bytes_per_ray
+        # bytes the launch physically moves: the input is read at ITS width (float64 rays: 64 B)
+        self.phys_bytes_per_ray = 8 * self.rays.element_size() + 8 * w * len(self.planes)
+        self.phys_bytes = self.n * self.phys_bytes_per_ray
         self._E = E
 
     def step(self):
@@ -130,9 +169,28 @@ class Workload:
         torch.cuda.synchronize()
         return ev0.elapsed_time(ev1) / steps, time.perf_counter() - t0
 
+    def e2e(self, reps=5):
+        """The drop-in call on device-resident rays: System.ray_trace(torch rays, m0, m1, dtype) -- lowering,
+        table keys, output allocation and the launch (ms per call, synchronised)."""
+        import torch
+        dt = "float32" if self.code != self._E.C.RTPB_F64 else None
+        del self.out                                        # System.ray_trace allocates its own history
+        torch.cuda.empty_cache()
+        h = self.system.ray_trace(self.rays, self.m0, self.m1, dtype=dt)
+        del h
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            h = self.system.ray_trace(self.rays, self.m0, self.m1, dtype=dt)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+            del h
+        return float(np.median(ts)) * 1e3
+
     def fill_rate(self):
         """The output buffer's delivered plain-write rate (GB/s, torch fill_): context for the history's
-        multi-plane write pattern, which is placement-sensitive."""
+        multi-plane write pattern."""
         import torch
         flat = self.out.view(-1)
         # chunks below 2^31 elements keep torch on its vectorised fill kernel
@@ -151,9 +209,7 @@ class Workload:
 
 def stream_copy_rate(device, nbytes=4 << 30, reps=10):
     """Measured copy rate of the device (GB/s, read + write bytes of a torch copy_ between two fresh
-    `nbytes` buffers): the measured stream-copy figure SURVEY §8(d) asks for beside the 8 TB/s spec.  It is
-    torch's elementwise copy kernel, not a tuned one (4.7 TB/s on MI355X, below the trace kernel's own
-    rate), so `frac` stays priced against the spec peak."""
+    `nbytes` buffers): the measured stream-copy figure SURVEY §8(d) asks for beside the 8 TB/s spec."""
     import torch
     src = torch.ones(nbytes // 8, dtype=torch.float64, device=device)
     dst = torch.empty_like(src)
@@ -252,56 +308,246 @@ def cpu_parallel(config, procs, secs=4.0):
             "sample": f"{label} split over {procs} processes, ~{secs:.0f} s each"}
 
 
-def measure_traffic(args, config):
-    """HBM bytes per trace launch from rocprofv3 PMC counters (separate child runs, FETCH_SIZE and
-    WRITE_SIZE in separate passes; gfx950: FETCH_SIZE counts half the bytes of wide streaming reads, so
-    it is doubled -- MI355X_MICROARCH.md §HBM)."""
+# ---------------------------------------------------------------------------------------------- PMC
+def _pmc_run(args, config, counters, kernel):
+    """One rocprofv3 --pmc child run of this script (--pmc-child --config CONFIG): per-dispatch counter
+    values of the kernels whose name contains `kernel` -> {counter: [values]} or an error string."""
+    import csv
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
+    d = os.path.join(ROOT, "gpurun_out", "bench_pmc", config, "_".join(counters))
+    shutil.rmtree(d, ignore_errors=True)
+    cmd = [prof, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", d, "-o", "pmc", "--",
+                                              sys.executable, os.path.abspath(__file__), "--pmc-child",
+                                              "--config", config, "--scale", str(args.scale), "--rays",
+                                              str(args.rays)]
+    try:
+        subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                       stdin=subprocess.DEVNULL, env=dict(os.environ, TMPDIR="/tmp"))
+    except Exception as e:  # noqa: BLE001
+        return None, f"rocprofv3 {counters} failed: {e}"
+    vals = {c: [] for c in counters}
+    for dp, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                with open(os.path.join(dp, f)) as fh:
+                    for row in csv.DictReader(fh):
+                        if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") in vals:
+                            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    if not all(vals.values()):
+        return None, f"no {counters} rows for {kernel}"
+    return vals, None
+
+
+def measure_traffic(args, config):
+    """HBM bytes per trace launch from rocprofv3 PMC counters (FETCH_SIZE and WRITE_SIZE in separate
+    passes; gfx950: FETCH_SIZE counts half the bytes of wide streaming reads, so it is doubled --
+    MI355X_MICROARCH.md §HBM).  Counters are in KiB."""
     out = {}
-    outdir = os.path.join(ROOT, "gpurun_out", "bench_pmc", config)
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(outdir, ctr)
-        shutil.rmtree(d, ignore_errors=True)
-        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", config,
-               "--scale", str(args.scale), "--rays", str(args.rays)]
-        try:
-            subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           env=dict(os.environ, TMPDIR="/tmp"))
-        except Exception as e:  # noqa: BLE001
-            return None, f"rocprofv3 {ctr} failed: {e}"
-        vals = []
-        for dp, _, files in os.walk(d):
-            for f in files:
-                if f.endswith("counter_collection.csv"):
-                    import csv
-                    with open(os.path.join(dp, f)) as fh:
-                        for row in csv.DictReader(fh):
-                            if "trace_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
-                                vals.append(float(row["Counter_Value"]))
-        if not vals:
-            return None, f"no {ctr} rows"
-        out[ctr] = float(np.median(vals))
-    # counters are in KiB units
+        vals, err = _pmc_run(args, config, [ctr], "trace_kernel")
+        if err:
+            return None, err
+        out[ctr] = float(np.median(vals[ctr]))
     return (2.0 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024.0, None
+
+
+F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+
+
+def measure_c5_flops(args):
+    """float64 FLOPs per ray of the fused sweep kernel from one PMC pass over a reduced C5 sweep (one field
+    point x 7 wavelengths x the full 10M-ray fan: the same per-ray work as the full sweep).  FLOPs =
+    64 lanes x (2 FMA + MUL + ADD + TRANS) per wave-instruction.  Also the VALU instructions per ray."""
+    vals, err = _pmc_run(args, "c5", list(F64_COUNTERS), "sweep_kernel")
+    if err:
+        return None, err
+    tot = {k: sum(v) for k, v in vals.items()}
+    flops = 64.0 * (2 * tot["SQ_INSTS_VALU_FMA_F64"] + tot["SQ_INSTS_VALU_MUL_F64"] + tot["SQ_INSTS_VALU_ADD_F64"] +
+                    tot["SQ_INSTS_VALU_TRANS_F64"])
+    rays = 7 * C5_FAN[0] * C5_FAN[1]
+    return {"flops_per_ray": flops / rays, "f64_wave_instructions": tot, "pmc_sample_rays": rays}, None
 
 
 def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None, copy=None):
     achieved = wl.alg_bytes / (kernel_ms * 1e-3) / 1e9
+    phys = wl.phys_bytes / (kernel_ms * 1e-3) / 1e9
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
          "traffic": traffic, "kernel": "trace_kernel", "kernel_ms_avg": kernel_ms,
          "kernel_ms_method": "HIP events on the launch stream around the K launches / K",
          "alg_bytes_per_launch": wl.alg_bytes, "alg_bytes_per_ray": wl.bytes_per_ray,
-         "alg_bytes_per_ray_surface": wl.bytes_per_ray / wl.S}
+         "alg_bytes_formula": "SURVEY.md 8(d) / BASELINE.md: 16 w (S+1) per ray, w = storage width",
+         "alg_bytes_per_ray_surface": wl.bytes_per_ray / wl.S,
+         "physical_bytes_per_launch": wl.phys_bytes, "physical_bytes_per_ray": wl.phys_bytes_per_ray,
+         "achieved_physical": phys, "frac_physical": phys / HBM_PEAK_GBS,
+         "physical_note": "the input rays are float64 (64 B read per ray); traffic (PMC) counts these bytes"}
     if fill:
-        r.update(output_fill_GBps=fill, frac_of_output_fill=achieved / fill)
+        r.update(output_fill_GBps=fill, frac_of_output_fill=phys / fill)
     if copy:
-        r.update(torch_copy_GBps=copy, frac_of_torch_copy=achieved / copy)
+        r.update(torch_copy_GBps=copy)
     if traffic_note:
         r["traffic_note"] = traffic_note
     return r
+
+
+# ---------------------------------------------------------------------------------------------- configs
+def _barrier(world):
+    import torch
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _gather(world, vals):
+    """[per-rank list of floats] (gloo all_gather; the control plane only)."""
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64)
+    if world == 1:
+        return [t.tolist()]
+    import torch.distributed as dist
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def run_c2(args, dev, copy):
+    import torch
+    w2 = Workload("c2", dev, 0, c2_rays=args.rays)
+    for _ in range(max(args.warmup, 5)):
+        w2.step()
+    torch.cuda.synchronize()
+    steps = max(args.steps, 50)
+    k2, e2 = w2.timed(steps)
+    tr2, note2 = (None, None)
+    if args.traffic == "auto":
+        tr2, note2 = measure_traffic(args, "c2")
+    res = {"baseline_config": "configs[1]", "workload": w2.workload, "dtype": "f64", "storage": w2.storage,
+           "value": w2.n * w2.S * steps / e2, "unit": UNIT, "n_gpus": 1, "steps": steps, "ms_per_step": e2 / steps * 1e3,
+           "rays": w2.n, "surfaces": w2.S, "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate(), copy)}
+    del w2
+    torch.cuda.empty_cache()
+    return res
+
+
+def run_c4(args, dev, rank, world, copy):
+    """BASELINE configs[3]: the 100M-ray OPM fan strong-scaled over the ranks (each rank its phi rows)."""
+    import torch
+    wl = Workload("c4", dev, rank, world=world, scale=args.scale)
+    for _ in range(max(2, min(args.warmup, 5))):
+        wl.step()
+    steps = max(3, min(args.steps, 20))
+    _barrier(world)
+    kernel_ms, wall = wl.timed(steps)
+    _barrier(world)
+    g = _gather(world, [wall, kernel_ms, float(wl.n)])
+    max_wall = max(x[0] for x in g)
+    res = None
+    if rank == 0:
+        traffic, note = (None, None)
+        if world == 1 and args.traffic == "auto":
+            traffic, note = measure_traffic(args, "c4")
+        per_rank = [{"rank": r, "rays": int(x[2]), "kernel_ms": x[1],
+                     "alg_GBps": x[2] * wl.bytes_per_ray / (x[1] * 1e-3) / 1e9,
+                     "frac_8TBs": x[2] * wl.bytes_per_ray / (x[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, "wall_s": x[0]}
+                    for r, x in enumerate(g)]
+        res = {"baseline_config": "configs[3]", "workload": wl.workload, "dtype": "f64", "storage": wl.storage,
+               "value": wl.total_rays * wl.S * steps / max_wall, "unit": UNIT, "n_gpus": world, "steps": steps,
+               "ms_per_step": max_wall / steps * 1e3, "scaling": "strong", "total_rays": wl.total_rays,
+               "surfaces": wl.S, "planes_stored": len(wl.planes),
+               "parallelism": f"phi-row ray shards x{world} (no collective)",
+               "roofline": roofline(wl, max(x[1] for x in g), traffic, note, wl.fill_rate() if world == 1 else None,
+                                    copy),
+               "per_rank": per_rank}
+        if world == 1:
+            res["roofline"]["note"] = "N=1: the whole 100M-ray fan on one GPU (80 GB in HBM)"
+    del wl
+    torch.cuda.empty_cache()
+    return res
+
+
+def run_c5(args, dev, rank, world):
+    """BASELINE configs[4]: the fused spot-diagram sweep, field points split over the ranks."""
+    import torch
+    import ray_trace_pb_amd.materials as mat
+    import ray_trace_pb_amd.raytrace as rt
+    from ray_trace_pb_amd import analysis
+    import systems
+    n_side = int(round(np.sqrt(args.c5_fields)))
+    fields = systems.c5_field_points(n_side)
+    f0, f1 = rt.shard_bounds(len(fields), world)[rank]
+    mine = fields[f0:f1]
+    system = systems.c5_system(rt, mat)
+    wls = systems.C5_WAVELENGTHS
+    theta = 0.5 * np.pi / 180
+    analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine[:1], wls, theta, 33, 32, device=dev)
+    kms, walls, hbm = [], [], 0.0
+    summ = None
+    for _ in range(args.c5_steps):
+        _barrier(world)
+        t0 = time.perf_counter()
+        summ, timing = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine, wls, theta, C5_FAN[0],
+                                           C5_FAN[1], device=dev)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        kms.append(sum(p["kernel_ms"] for p in timing["per_device"]))
+        hbm = sum(p["hbm_bytes"] for p in timing["per_device"])
+    _barrier(world)
+    my_rays = float(len(mine) * len(wls) * C5_FAN[0] * C5_FAN[1])
+    g = _gather(world, [float(np.median(walls)), float(np.median(kms)), my_rays, hbm])
+    if rank != 0:
+        return None
+    S = len(system.surfaces)
+    total = sum(x[2] for x in g)
+    max_wall = max(x[0] for x in g)
+    kmax = max(x[1] for x in g)
+    per_rank = [{"rank": r, "rays": int(x[2]), "kernel_ms": x[1], "hbm_bytes": x[3],
+                 "hbm_GBps": x[3] / (x[1] * 1e-3) / 1e9} for r, x in enumerate(g)]
+    res = {"baseline_config": "configs[4]", "workload": (
+        f"C5: spot-diagram sweep of scripts/2021_10_06_ray_trace_system.py:120-145,186 (ODT excitation path, "
+        f"4 doublets + PerfectLens + flat, S=14), {len(fields)} field points x {len(wls)} wavelengths x "
+        f"get_ray_fan(0.5 deg, {C5_FAN[0]}, nphis={C5_FAN[1]}), final plane reduced to per-group spot statistics "
+        f"in the fused sweep kernel"), "dtype": "f64", "value": total * S / max_wall, "unit": UNIT,
+        "n_gpus": world, "steps": args.c5_steps, "ms_per_step": max_wall * 1e3, "scaling": "strong",
+        "total_rays": int(total), "surfaces": S, "parallelism": f"field-point shards x{world} (no collective)",
+        "per_rank": per_rank,
+        "rms_radius_um_field0": (summ["rms_radius"][0] * 1e3).tolist() if rank == 0 else None}
+    rl = {"bound": "valu_f64", "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "sweep_kernel",
+          "kernel_ms_max_rank": kmax, "hbm_GBps_max_rank": max(p["hbm_GBps"] for p in per_rank),
+          "hbm_note": "the rays never leave registers: HBM carries only the per-tile partial sums"}
+    if world == 1 and args.traffic == "auto":
+        fl, err = measure_c5_flops(args)
+        if fl:
+            rays0 = g[0][2]
+            rl.update(achieved=fl["flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
+                      flops_per_ray=fl["flops_per_ray"], f64_wave_instructions_sample=fl["f64_wave_instructions"],
+                      pmc_sample_rays=fl["pmc_sample_rays"],
+                      flops_method="PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes (FMA = 2) on a 1-field "
+                                   "sweep, scaled per ray")
+            rl["frac"] = rl["achieved"] / F64_VALU_PEAK_TFLOPS
+        else:
+            rl["flops_note"] = err
+    res["roofline"] = rl
+    return res
+
+
+def pmc_child(args, dev):
+    """Target of the rocprofv3 --pmc child runs: a few launches of one config's kernel."""
+    import torch
+    if args.config == "c5":
+        import ray_trace_pb_amd.materials as mat
+        import ray_trace_pb_amd.raytrace as rt
+        from ray_trace_pb_amd import analysis
+        import systems
+        analysis.spot_sweep(systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1),
+                            systems.c5_field_points(8)[:1], systems.C5_WAVELENGTHS, 0.5 * np.pi / 180, C5_FAN[0],
+                            C5_FAN[1], device=dev)
+    else:
+        wl = Workload(args.config, dev, 0, scale=args.scale, c2_rays=args.rays)
+        for _ in range(3):
+            wl.step()
+    torch.cuda.synchronize()
 
 
 def main():
@@ -312,89 +558,94 @@ def main():
     # one GPU per rank; the modulo only matters when rehearsing several ranks on one GPU
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
+    if args.pmc_child:
+        pmc_child(args, dev)
+        return
     if world > 1:
         # Control plane only (barriers, max-reduction of the step time, per-rank kernel times): rays are
         # independent, so the trace has no data-path exchange and needs no RCCL communicator.
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
-    wl = Workload(args.config, dev, rank, scale=args.scale, c2_rays=args.rays)
-    if args.pmc_child:
-        for _ in range(3):
-            wl.step()
-        torch.cuda.synchronize()
-        return
-
+    _log(f"rank {rank}/{world}: headline {args.config}")
+    wl = Workload(args.config, dev, rank, world=1, scale=args.scale, c2_rays=args.rays)
     for _ in range(args.warmup):
         wl.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # each rank's own clock stops at its device sync; the job time is the max over ranks (all_reduce
-    # below), so the closing barrier's own latency is not charged to the K steps
+    _barrier(world)
+    # each rank's own clock stops at its device sync; the job time is the max over ranks (gathered below),
+    # so the closing barrier's own latency is not charged to the K steps
     kernel_ms, elapsed = wl.timed(args.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    _barrier(world)
     fill = wl.fill_rate() if rank == 0 else None
-    copy = stream_copy_rate(dev) if rank == 0 else None
-
-    per_rank = None
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
-        gathered = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(gathered, t)
-        per_rank = [{"rank": r, "kernel_ms": float(g[1]), "GBps": wl.alg_bytes / (float(g[1]) * 1e-3) / 1e9,
-                     "wall_s": float(g[0])} for r, g in enumerate(gathered)]
-        elapsed = max(p["wall_s"] for p in per_rank)
-        kernel_ms_max = max(p["kernel_ms"] for p in per_rank)
-    else:
-        kernel_ms_max = kernel_ms
-
+    e2e_ms = wl.e2e() if args.config == "c3" else None
+    g = _gather(world, [elapsed, kernel_ms])
+    per_rank = [{"rank": r, "kernel_ms": x[1], "alg_GBps": wl.alg_bytes / (x[1] * 1e-3) / 1e9, "wall_s": x[0]}
+                for r, x in enumerate(g)]
+    elapsed = max(p["wall_s"] for p in per_rank)
+    kernel_ms_max = max(p["kernel_ms"] for p in per_rank)
     total_units = world * wl.n * wl.S * args.steps
     value = total_units / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    head = wl
+    del wl
+    torch.cuda.empty_cache()
+    copy = stream_copy_rate(dev) if rank == 0 else None
 
+    line = None
     if rank == 0:
         traffic, note = (None, None)
         if world == 1 and args.traffic == "auto":
+            _log("PMC traffic of the headline kernel")
             traffic, note = measure_traffic(args, args.config)
-        rl = roofline(wl, kernel_ms_max, traffic, note, fill, copy)
+        rl = roofline(head, kernel_ms_max, traffic, note, fill, copy)
         rl["kernel_ms_max_rank"] = kernel_ms_max
         line = {
             "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": wl.workload, "storage": wl.storage, "rays_per_gpu": wl.n, "surfaces": wl.S,
-                       "planes_stored": len(wl.planes), "layout": "aos",
+            "vs_baseline": None, "dtype": "f64", "storage_dtype": "f32" if head.code != 0 else "f64",
+            "data": "synthetic",
+            "config": {"workload": head.workload, "baseline_config": "configs[2]" if args.config == "c3" else None,
+                       "storage": head.storage, "rays_per_gpu": head.n, "surfaces": head.S,
+                       "planes_stored": len(head.planes), "layout": "aos",
                        "parallelism": f"ray shards x{world} (no collective)"},
             "roofline": rl,
         }
-        if per_rank:
+        if e2e_ms is not None:
+            line["e2e_ms"] = e2e_ms
+            line["e2e_over_kernel"] = e2e_ms / kernel_ms
+            line["e2e_note"] = ("System.ray_trace(torch rays, Vacuum(), Vacuum(), dtype='float32') on the device-"
+                                "resident C3 bundle: lowering, Ebaf11 table keys (the previous bundle's, checked "
+                                "by the kernel's table-miss flag), history allocation, launch, synchronise")
+        if world > 1:
             line["per_rank"] = per_rank
-        if world == 1 and args.secondary == "auto" and args.config != "c2":
-            del wl
-            torch.cuda.empty_cache()
-            w2 = Workload("c2", dev, 0, c2_rays=args.rays)
-            for _ in range(max(args.warmup, 5)):
-                w2.step()
-            torch.cuda.synchronize()
-            k2, e2 = w2.timed(max(args.steps, 50))
-            tr2, note2 = (None, None)
-            if args.traffic == "auto":
-                tr2, note2 = measure_traffic(args, "c2")
-            line["secondary"] = {"config": "BASELINE configs[1]: " + w2.workload, "dtype": "f64",
-                                 "value": w2.n * w2.S * max(args.steps, 50) / e2, "unit": UNIT,
-                                 "rays": w2.n, "surfaces": w2.S,
-                                 "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate(), copy)}
+    del head
+
+    configs = [c for c in args.configs.split(",") if c and c != "none"]
+    others = {}
+    if "c2" in configs and world == 1 and rank == 0:
+        _log("configs[1] c2")
+        others["c2"] = run_c2(args, dev, copy)
+    if "c4" in configs and args.config != "c4":
+        _log(f"rank {rank}: configs[3] c4")
+        r = run_c4(args, dev, rank, world, copy)
+        if rank == 0:
+            others["c4"] = r
+    if "c5" in configs:
+        _log(f"rank {rank}: configs[4] c5")
+        r = run_c5(args, dev, rank, world)
+        if rank == 0:
+            others["c5"] = r
+
+    if rank == 0:
+        line["configs"] = others
         if world == 1 and args.cpu_baseline == "auto":
-            cpu = cpu_time(args.config, 8.0)
+            _log("cpu baseline")
+            cpu = cpu_time(args.config if args.config != "c4" else "c3", 8.0)
             cpu["cpu_model"] = cpu_model()
             try:
                 # the GPU box allots 16 host CPUs per GPU; os.cpu_count() there reports the whole machine
                 procs = max(1, min(16, len(os.sched_getaffinity(0))))
-                cpu["parallel"] = cpu_parallel(args.config, procs)
+                cpu["parallel"] = cpu_parallel("c3", procs)
             except Exception as e:  # noqa: BLE001 -- the single-process baseline stands on its own
                 cpu["parallel"] = {"error": repr(e)}
             cpu["c1"] = cpu_time("c1", 2.0)
@@ -405,6 +656,7 @@ def main():
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -39,8 +39,9 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 3   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
-                                3: input element type separate from the storage type (in_dtype) */
+#define RTPB_ABI_VERSION 4   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+                                3: input element type separate from the storage type (in_dtype)
+                                4: + rtpb_trace_checked (table-miss flag) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -140,6 +141,16 @@ int rtpb_trace(const rtpb_plan* plan, int32_t device,
                const void* rays_in, int32_t in_dtype, int64_t n_rays, int32_t in_layout, int64_t in_field_stride,
                void* out, int32_t out_layout, int64_t out_plane_stride, int64_t out_field_stride,
                uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream);
+/* rtpb_trace plus a table-miss flag: `table_miss` (device pointer to one int32, may be NULL) is set to
+   1 by the launch when some ray's wavelength is not a key of some RTPB_TABLE material of the plan (that
+   ray's n would be NaN, unlike the material's own n()).  The caller zeroes it before the call and reads
+   it after the stream has completed.  Lets a caller trace optimistically with the table keys of a
+   previous bundle and re-trace with the bundle's own keys only on a miss (bit-identical either way). */
+int rtpb_trace_checked(const rtpb_plan* plan, int32_t device,
+                       const void* rays_in, int32_t in_dtype, int64_t n_rays, int32_t in_layout,
+                       int64_t in_field_stride, void* out, int32_t out_layout, int64_t out_plane_stride,
+                       int64_t out_field_stride, uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream,
+                       int32_t* table_miss);
 
 /* ---- tracing host buffers (NumPy in, NumPy out), sharded over several GPUs ------------------ */
 /* rays_in: host, n_rays x 8 AOS of `in_dtype`.  out: host, nslots x n_rays x 8 AOS of the plan's dtype

@@ -11,7 +11,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 3
+RTPB_ABI_VERSION = 4
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
@@ -56,6 +56,8 @@ SIGNATURES = {
                                         ctypes.POINTER(_P)]),
     "rtpb_plan_destroy": (ctypes.c_int, [_P]),
     "rtpb_trace": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P]),
+    "rtpb_trace_checked": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P,
+                                          _P]),
     "rtpb_trace_host": (ctypes.c_int, [_P, _P, _i32, _i64, _P, _u64, _u64, ctypes.POINTER(_i32), _i32]),
     "rtpb_ray_fan": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, ctypes.POINTER(_dbl),
                                     _dbl, _P]),

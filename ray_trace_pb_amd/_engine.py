@@ -100,11 +100,16 @@ def _distinct_device(col):
     import torch
     if col.dtype not in (torch.float64, torch.float32):
         col = col.double()
+    if col.shape[0] == 0:
+        return np.empty(0)
+    if col.stride(0) == 0:
+        # a broadcast column (e.g. rays = ray.expand(N, 8)): every element is the one stored value
+        return np.unique(col[:1].double().cpu().numpy())
     ws = torch.empty(DISTINCT_SLOTS + 1, dtype=torch.int64, device=col.device)
     lib = C.lib()
     C.check(lib.rtpb_distinct_keys(col.device.index, col.data_ptr(),
                                    C.RTPB_F32 if col.dtype == torch.float32 else C.RTPB_F64, col.shape[0],
-                                   max(col.stride(0), 1), ws.data_ptr(), DISTINCT_SLOTS, DISTINCT_MAX_KEYS,
+                                   col.stride(0), ws.data_ptr(), DISTINCT_SLOTS, DISTINCT_MAX_KEYS,
                                    ws.data_ptr() + 8 * DISTINCT_SLOTS, torch.cuda.current_stream(col.device).cuda_stream))
     host = ws.cpu().numpy()
     if int(host[-1] & 0xFFFFFFFF) > DISTINCT_MAX_KEYS:
@@ -128,6 +133,65 @@ def distinct_wavelengths(col):
     if w.size and (w == w[0]).all():
         return w[:1].copy()
     return np.unique(w)
+
+
+# ------------------------------------------------------------------------- table keys of previous bundles
+# Materials that lower to host-evaluated tables (user Material subclasses, Ebaf11) need the bundle's
+# distinct wavelengths -- a pass over the whole wavelength column (rtpb_distinct_keys) before every trace.
+# Torch-CUDA callers trace optimistically instead: with the key set of the previous bundle traced through
+# the same tabulated materials, checked by the kernel (rtpb_trace_checked's table-miss flag), and only on a
+# miss is the column scanned and the bundle re-traced with its own keys.  Exact either way: a table holds
+# n() of the material at each key, and every ray's key is present or the trace is redone.  Assumes n()
+# depends only on the wavelength and the material's attributes (the fingerprint below).
+_KEYS = collections.OrderedDict()
+_KEYS_MAX = 64
+
+
+class _NoFingerprint(Exception):
+    pass
+
+
+def _fp(v, depth=0):
+    if depth > 8:
+        raise _NoFingerprint
+    if v is None or isinstance(v, (bool, int, float, complex, str, bytes, np.generic)):
+        return (type(v).__name__, v)
+    if isinstance(v, np.ndarray):
+        return ("nd", v.dtype.str, v.shape, v.tobytes())
+    if isinstance(v, (list, tuple)):
+        return (type(v).__name__,) + tuple(_fp(x, depth + 1) for x in v)
+    if isinstance(v, dict):
+        return ("dict",) + tuple(sorted((str(k), _fp(x, depth + 1)) for k, x in v.items()))
+    raise _NoFingerprint
+
+
+def tabulated(materials):
+    """The materials that lower to host-evaluated (wavelength, n) tables."""
+    return [m for m in materials if not (hasattr(m, "_rtpb_lower") and m._rtpb_lower() is not None)]
+
+
+def table_fingerprint(materials):
+    """Hashable identity of the tabulated materials' n() (class + attribute values), or None."""
+    try:
+        return tuple((type(m).__module__, type(m).__qualname__, id(type(m)), _fp(vars(m))) for m in materials)
+    except (_NoFingerprint, TypeError):
+        return None
+
+
+def previous_keys(fp):
+    keys = _KEYS.get(fp) if fp is not None else None
+    if keys is not None:
+        _KEYS.move_to_end(fp)
+    return keys
+
+
+def remember_keys(fp, keys):
+    if fp is None:
+        return
+    _KEYS[fp] = keys
+    _KEYS.move_to_end(fp)
+    while len(_KEYS) > _KEYS_MAX:
+        _KEYS.popitem(last=False)
 
 
 def lower_material(m, wavelengths):
@@ -296,9 +360,10 @@ def trace_host(low, rays2d, planes, devices=None, out=None):
     return out
 
 
-def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None):
+def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None, miss=None):
     """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA] of the
-    plan's storage type."""
+    plan's storage type.  ``miss``: a zeroed int32 CUDA tensor the launch sets to 1 when a ray's
+    wavelength is not a key of the plan's TABLE materials (rtpb_trace_checked)."""
     import torch
     tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
     in_code = input_code(rays.dtype)
@@ -311,6 +376,11 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     if stream is None:
         stream = torch.cuda.current_stream(rays.device).cuda_stream
     with plan_ref(low) as plan:
-        C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
-                                   out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+        if miss is None:
+            C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
+                                       out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+        else:
+            C.check(C.lib().rtpb_trace_checked(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
+                                               0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream,
+                                               miss.data_ptr()))
     return out

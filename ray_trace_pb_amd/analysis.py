@@ -36,13 +36,15 @@ def spot_stats_raw(plane, group_size, stream=None):
 
 
 def summarize(raw):
-    """count, centroid (x, y, z) and RMS spot radius about the centroid from the raw sums."""
+    """count, centroid (x, y, z) and RMS spot radius about the centroid from the raw sums (kept as
+    "raw": count, sum x, y, z, x^2, y^2, xy per group, reduced in the kernels' fixed order)."""
     raw = np.asarray(raw, dtype=np.float64)
     n = raw[..., 0]
     with np.errstate(invalid="ignore", divide="ignore"):
         cx, cy, cz = raw[..., 1] / n, raw[..., 2] / n, raw[..., 3] / n
         var = raw[..., 4] / n - cx * cx + raw[..., 5] / n - cy * cy
-    return {"count": n, "centroid": np.stack((cx, cy, cz), axis=-1), "rms_radius": np.sqrt(np.maximum(var, 0.0))}
+    return {"count": n, "centroid": np.stack((cx, cy, cz), axis=-1), "rms_radius": np.sqrt(np.maximum(var, 0.0)),
+            "raw": raw}
 
 
 def spot_stats(plane, group_size):

@@ -71,6 +71,7 @@ struct TraceArgs {
     const DevMaterial<double>* __restrict__ mats;
     const double* __restrict__ table;
     const double* __restrict__ itab;   // indexed materials: [nkeys keys][(nsurf+1) x nkeys values]
+    int32_t* miss;        // rtpb_trace_checked: set to 1 when a ray's wavelength is no TABLE key (or NULL)
     int64_t n;
     int64_t in_fs;        // SOA input field stride
     int64_t out_ps;       // output plane (slot) stride

@@ -215,10 +215,10 @@ RTPB_HD Rcp<T> host_rcp(T b, T y, bool ok) {
     return Rcp<T>{b, y, ok};
 }
 
-// host: the range test of fastdiv_den_ok
+// host: the range test of fastdiv_den_ok, exactly (2^-120 <= |b| < 2^120, or 0, inf, NaN)
 inline bool host_rcp_ok(double b) {
     const double m = std::fabs(b);
-    return (m >= 0x1p-120 && m <= 0x1p120) || b == 0.0 || std::isinf(b) || std::isnan(b);
+    return (m >= 0x1p-120 && m < 0x1p120) || b == 0.0 || std::isinf(b) || std::isnan(b);
 }
 
 template <typename T>
@@ -343,6 +343,21 @@ RTPB_HD T material_n(const DevMaterial<T>& m, T wl, TablePtr table, G* g = nullp
         return (lo < len && T(table[2 * (off + lo)]) == wl) ? T(table[2 * (off + lo) + 1]) : qnan<T>();
     }
     }
+}
+
+// Whether wl is a key of TABLE material m (the same search and matching rule as material_n's TABLE case:
+// NaN finds a NaN key).  A ray whose wavelength is no key would get n = NaN from the table.
+template <typename T, typename TablePtr>
+RTPB_HD bool table_has_key(const DevMaterial<T>& m, T wl, TablePtr table) {
+    const int len = m.table_len, off = m.table_off;
+    if (is_nan(wl)) return len > 0 && is_nan(T(table[2 * (off + len - 1)]));
+    int lo = 0, hi = len;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (T(table[2 * (off + mid)]) < wl) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < len && T(table[2 * (off + lo)]) == wl;
 }
 
 // ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)

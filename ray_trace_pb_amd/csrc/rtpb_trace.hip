@@ -30,7 +30,8 @@ thread_local TimingState g_timing;
 
 
 int trace_impl(rtpb_plan* plan, int dev, const void* in, int in_dtype, int64_t n, int il, int64_t in_fs, void* out,
-               int ol, int64_t out_ps, int64_t out_fs, uint64_t lo, uint64_t hi, hipStream_t st) {
+               int ol, int64_t out_ps, int64_t out_fs, uint64_t lo, uint64_t hi, hipStream_t st,
+               int32_t* miss = nullptr) {
     void* blob = nullptr;
     int rc = plan_device_blob(plan, dev, &blob);
     if (rc) return rc;
@@ -45,6 +46,7 @@ int trace_impl(rtpb_plan* plan, int dev, const void* in, int in_dtype, int64_t n
         a.mats = reinterpret_cast<const DevMaterial<double>*>(static_cast<char*>(blob) + plan->off_mats);
         a.table = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_table);
         a.itab = reinterpret_cast<const double*>(static_cast<char*>(blob) + plan->off_itab);
+        a.miss = miss;
         a.n = n;
         a.in_fs = in_fs;
         a.out_ps = out_ps;
@@ -246,6 +248,14 @@ int rtpb_shutdown(void) {
 int rtpb_trace(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int32_t in_dtype, int64_t n_rays,
                int32_t in_layout, int64_t in_field_stride, void* out, int32_t out_layout, int64_t out_plane_stride,
                int64_t out_field_stride, uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream) {
+    return rtpb_trace_checked(plan_c, device, rays_in, in_dtype, n_rays, in_layout, in_field_stride, out, out_layout,
+                              out_plane_stride, out_field_stride, plane_mask_lo, plane_mask_hi, stream, nullptr);
+}
+
+int rtpb_trace_checked(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int32_t in_dtype,
+                       int64_t n_rays, int32_t in_layout, int64_t in_field_stride, void* out, int32_t out_layout,
+                       int64_t out_plane_stride, int64_t out_field_stride, uint64_t plane_mask_lo,
+                       uint64_t plane_mask_hi, void* stream, int32_t* table_miss) {
     auto* plan = const_cast<rtpb_plan*>(plan_c);
     if (!plan) return fail(RTPB_E_INVALID, "plan is NULL");
     int rc = check_device(device);
@@ -273,7 +283,8 @@ int rtpb_trace(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int
     if (out_layout == RTPB_SOA && out_field_stride < n_rays) return fail(RTPB_E_INVALID, "out_field_stride < n_rays");
     DeviceGuard g(device);
     return trace_impl(plan, device, rays_in, in_dtype, n_rays, in_layout, in_field_stride, out, out_layout,
-                      out_plane_stride, out_field_stride, plane_mask_lo, plane_mask_hi, static_cast<hipStream_t>(stream));
+                      out_plane_stride, out_field_stride, plane_mask_lo, plane_mask_hi, static_cast<hipStream_t>(stream),
+                      table_miss);
 }
 
 int rtpb_trace_host(const rtpb_plan* plan_c, const void* rays_in, int32_t in_dtype, int64_t n_rays, void* out,

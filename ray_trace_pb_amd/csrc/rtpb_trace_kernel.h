@@ -98,6 +98,24 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     // indexed materials: the ray's key once (-1 = wavelength not among the plan's keys: every material
     // is then evaluated as without the index, TABLE materials giving NaN as a table miss does)
     const int widx = kIdx ? key_index(lds_table, a.nkeys, wl0) : -1;
+    if constexpr (kIdx || kTabLds || kTabGlobal) {
+        // rtpb_trace_checked: flag rays whose wavelength is not a table key (wave-uniform pointer test;
+        // every flagging lane stores the same value, so no atomic is needed)
+        if (a.miss != nullptr) {
+            bool miss = false;
+            if constexpr (kIdx) {
+                miss = widx < 0;
+            } else {
+                for (int k = 0; k <= a.nsurf; ++k) {
+                    const DevMaterial<T> m = load_material<T>(mats + k);
+                    if (m.kind == TABLE)
+                        miss = miss || !(kTabLds ? table_has_key(m, wl0, static_cast<const double*>(lds_table))
+                                                 : table_has_key(m, wl0, table));
+                }
+            }
+            if (valid && miss) a.miss[0] = 1;
+        }
+    }
     auto mat_n = [&](cptr<DevMaterial<T>> mp) -> T {
         if constexpr (kIdx) {
             if (widx >= 0) return lds_table[a.nkeys * (1 + static_cast<int>(mp - mats)) + widx];

@@ -388,18 +388,14 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     full = isinstance(planes, str) and planes == "all"
     last = rays[-1]
 
+    layout_code = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
+    if on_device:
+        return _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code)
+
     def wavelengths():
         return E.distinct_wavelengths(last[:, 7])
 
     low = E.lower(surfaces, materials, wavelengths, code)
-    layout_code = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
-    if on_device:
-        if full and k > 1:
-            import torch
-            new = E.trace_device(low, last, sel[1:])
-            return torch.cat((rays.to(new.dtype), new), dim=0)
-        out = E.trace_device(low, last, sel, layout_out=layout_code)
-        return out
     if layout != "aos":
         raise ValueError("layout='soa' is only available for device (torch CUDA) inputs")
     devs = _resolve_devices(devices)
@@ -409,6 +405,37 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
         E.trace_host(low, last, sel[1:], devs, out=out[k:])
         return out
     return E.trace_host(low, last, sel, devs)
+
+
+def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code):
+    """The torch-CUDA trace of trace_surfaces.  Tabulated materials (user n() overrides, Ebaf11) are
+    lowered with the key set of the previous bundle traced through them when there is one, and the kernel
+    flags any ray whose wavelength is not among those keys (rtpb_trace_checked); only then is the bundle's
+    wavelength column scanned (rtpb_distinct_keys) and the bundle re-traced with its own keys.  Either
+    way every ray reads n() of its own wavelength: bit-identical to lowering with the bundle's keys."""
+    import torch
+    k = rays.shape[0]
+
+    def run(low, miss=None):
+        if full and k > 1:
+            new = E.trace_device(low, last, sel[1:], miss=miss)
+            return torch.cat((rays.to(new.dtype), new), dim=0)
+        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss)
+
+    tab = E.tabulated(materials)
+    if not tab:
+        return run(E.lower(surfaces, materials, None, code))
+    fp = E.table_fingerprint(tab)
+    prev = E.previous_keys(fp)
+    if prev is not None:
+        miss = torch.zeros(1, dtype=torch.int32, device=last.device)
+        out = run(E.lower(surfaces, materials, lambda: prev, code), miss)
+        if int(miss.item()) == 0:
+            return out
+        del out
+    keys = E.distinct_wavelengths(last[:, 7])
+    E.remember_keys(fp, keys)
+    return run(E.lower(surfaces, materials, lambda: keys, code))
 
 
 def _trace_scattered(surfaces, materials, rays, devs, *, planes, dtype, layout, gather):
@@ -681,13 +708,14 @@ class System:
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
                                   layout=layout, gather=gather)
-        if _is_shard_list(rays):
-            return [self.ray_trace(r, initial_material, final_material, dtype=dtype) for r in rays]
         # user surfaces (own propagate, or own geometry hooks): run maximal runs of built-in surfaces
         # as fused GPU traces and hand the growing history to each user surface in between
         # (RT:658-659 order)
         if not (isinstance(planes, str) and planes == "all") or layout != "aos":
             raise ValueError("systems with user-defined surfaces support only planes='all', layout='aos'")
+        if _is_shard_list(rays):
+            return [self.ray_trace(r, initial_material, final_material, planes=planes, dtype=dtype, layout=layout)
+                    for r in rays]
         hist, i, S = rays, 0, len(self.surfaces)
         while i < S:
             if custom[i]:

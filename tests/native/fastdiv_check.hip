@@ -38,7 +38,7 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[6 * n + i] = tsqrt<double>(bi);
     out[7 * n + i] = tsqrt<double>(ai);
     const double mb = fabs(bi);          // host_rcp_ok (rtpb_math.h), the flag lower_surface stores
-    const bool ok = (mb >= 0x1p-120 && mb <= 0x1p120) || bi == 0.0 || isinf(bi) || isnan(bi);
+    const bool ok = (mb >= 0x1p-120 && mb < 0x1p120) || bi == 0.0 || isinf(bi) || isnan(bi);
     out[8 * n + i] = div1(ai, host_rcp(bi, yh[i], ok));
     GuardDefer g1, g2, g3, g4;
     out[9 * n + i] = div1(ai, r, &g1);

@@ -1,5 +1,6 @@
 """bench.py contract on the CPU: the roofline object's fields and the algorithmic-byte accounting of the
-headline workload.  The timed run itself needs a GPU (driver / gpurun)."""
+BASELINE configs (16 w (S+1) bytes per ray of a full history).
+The timed run itself needs a GPU (driver / gpurun)."""
 import types
 
 import bench
@@ -9,21 +10,32 @@ def test_c3_workload_size_and_bytes():
     nt, nph = bench.C3_FAN
     rays = 5 * nt * nph                                  # 5 field points x get_ray_fan(h, 1 deg, 3163, nphis=3162)
     assert rays == 50_007_030
-    S, planes = 9, 19
-    per_ray = 8 * 8 + planes * 8 * 4                     # float64 input record + 19 float32 history records
-    assert per_ray == 672
-    assert rays * per_ray == 33_604_724_160              # alg_bytes_per_launch in profiles/r02/bench.log
-    assert abs(per_ray / S - 74.667) < 1e-3
+    S, planes, w = 9, 19, 4
+    contract = 16 * w * (S + 1)                          # one float32 input record + 19 float32 planes
+    assert contract == 640 == 8 * w * (1 + planes)
+    physical = 8 * 8 + planes * 8 * w                    # the input is read as float64
+    assert physical == 672
+    assert rays * physical == 33_604_724_160             # physical bytes per launch (PMC traffic: +0.0 %)
+    assert rays * contract == 32_004_499_200
+
+
+def test_c4_c5_sizes():
+    nt, nph = bench.C4_FAN
+    assert nt * nph == 100_010_000
+    assert 16 * 4 * (11 + 1) * nt * nph == 76_807_680_000      # contract bytes of the 23-plane float32 history
+    assert 64 * 7 * bench.C5_FAN[0] * bench.C5_FAN[1] == 4_480_629_888
 
 
 def test_roofline_object_fields():
-    wl = types.SimpleNamespace(alg_bytes=33_604_724_160, bytes_per_ray=672, S=9)
+    wl = types.SimpleNamespace(alg_bytes=32_004_499_200, bytes_per_ray=640, S=9, phys_bytes=33_604_724_160,
+                               phys_bytes_per_ray=672)
     r = bench.roofline(wl, 6.2, traffic=3.36e10, traffic_note=None, fill=6800.0, copy=4700.0)
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
-    assert abs(r["achieved"] - 33_604_724_160 / 6.2e-3 / 1e9) < 1e-6
+    assert abs(r["achieved"] - 32_004_499_200 / 6.2e-3 / 1e9) < 1e-6
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12
-    assert abs(r["frac_of_output_fill"] - r["achieved"] / 6800.0) < 1e-12
-    assert abs(r["frac_of_torch_copy"] - r["achieved"] / 4700.0) < 1e-12
+    assert abs(r["achieved_physical"] - 33_604_724_160 / 6.2e-3 / 1e9) < 1e-6
+    assert abs(r["frac_of_output_fill"] - r["achieved_physical"] / 6800.0) < 1e-12
+    assert r["torch_copy_GBps"] == 4700.0
     assert "torch_copy_GBps" not in bench.roofline(wl, 6.2)

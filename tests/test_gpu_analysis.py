@@ -224,3 +224,77 @@ def test_spot_sweep_over_devices_is_bitwise_equal():
         assert [p["device"] for p in tm["per_device"]] == devs
         assert sum(p["rays"] for p in tm["per_device"]) == t1["rays"]
         assert all(p["kernel_ms"] > 0 for p in tm["per_device"])
+
+
+def fixed_order_sums(plane, group_size, tile=256):
+    """The spot kernels' reduction restated in NumPy, operation for operation (csrc/rtpb_analysis.hip
+    spot_partial_kernel / sweep_kernel + spot_final_kernel): per 256-ray tile a pairwise tree
+    (red[t] += red[t + w], w = 128 ... 1) of (1, x, y, z, x*x, y*y, x*y) over rays with finite x and y;
+    per group, thread t adds tiles t, t + 256, ... in order, then the same tree over the 256 threads."""
+    p = np.asarray(plane, dtype=np.float64).reshape(-1, group_size, plane.shape[-1])
+    G = p.shape[0]
+    tiles = -(-group_size // tile)
+    x, y, z = p[..., 0], p[..., 1], p[..., 2]
+    with np.errstate(invalid="ignore"):
+        ok = (x - x == 0.0) & (y - y == 0.0)
+    v = np.zeros((G, tiles * tile, 7))
+    with np.errstate(invalid="ignore", over="ignore"):
+        terms = np.stack((np.ones_like(x), x, y, z, x * x, y * y, x * y), -1)
+    v[:, :group_size] = np.where(ok[..., None], terms, 0.0)
+    v = v.reshape(G, tiles, tile, 7)
+    w = tile // 2
+    while w:
+        v[:, :, :w] = v[:, :, :w] + v[:, :, w:2 * w]
+        w //= 2
+    part = v[:, :, 0]                                            # (G, tiles, 7)
+    acc = np.zeros((G, tile, 7))
+    for c in range(0, tiles, tile):
+        blk = part[:, c:c + tile]
+        acc[:, :blk.shape[1]] = acc[:, :blk.shape[1]] + blk
+    w = tile // 2
+    while w:
+        acc[:, :w] = acc[:, :w] + acc[:, w:2 * w]
+        w //= 2
+    return acc[:, 0]
+
+
+def test_spot_stats_bitwise_vs_fixed_order_oracle():
+    """rtpb_spot_stats: every raw sum bit-identical to the NumPy restatement of its reduction order, with
+    ragged groups and more than 256 tiles per group (the second stage's sequential chains)."""
+    rng = np.random.default_rng(8)
+    G, per = 3, 256 * 300 + 77
+    plane = rng.normal(size=(G * per, 8)) * np.array([1, 2, 3, 1, 1, 1, 1, 1]) + 5.0
+    plane[rng.random(G * per) < 0.1, 0] = np.nan
+    plane[rng.random(G * per) < 0.01, 1] = np.inf
+    raw = analysis.spot_stats_raw(torch.from_numpy(plane).to(DEV), per).cpu().numpy()
+    assert np.array_equal(raw, fixed_order_sums(plane, per))
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_spot_sweep_sums_bitwise_vs_oracle(dtype):
+    """The fused C5 sweep (BASELINE configs[4] system: fan generation + trace + reduction in one kernel)
+    against the oracle: each group's fan from the reference generator, traced by the NumPy oracle, final
+    plane (rounded to the storage type) reduced in the kernel's order -- count and every sum bit for bit,
+    hence identical centroids and RMS radii.  Groups of 301 x 300 rays: 353 tiles, a ragged last tile."""
+    system = systems.c5_system(rt, mat)
+    fields = systems.c5_field_points(2)[1:3]
+    wls = [0.405, 0.635]
+    theta, nt, nph = 0.5 * np.pi / 180, 301, 300
+    summ, _ = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields, wls, theta, nt, nph,
+                                  device=DEV, dtype=dtype)
+    S = [surface_to_dict(s) for s in system.surfaces]
+    M = [material_to_dict(m) for m in [mat.Constant(1)] + list(system.materials) + [mat.Constant(1)]]
+    finals = []
+    for f in fields:
+        for w in wls:
+            rays = rt.get_ray_fan(f, theta, nt, w, nphis=nph)
+            if dtype == "float32":
+                rays = rays.astype(np.float32).astype(np.float64)
+            fin = O.ray_trace(S, M, rays)[-1]
+            finals.append(fin.astype(np.float32).astype(np.float64) if dtype == "float32" else fin)
+    ref = fixed_order_sums(np.concatenate(finals), nt * nph).reshape(len(fields), len(wls), 7)
+    assert np.array_equal(summ["raw"], ref)
+    assert summ["count"].min() > 0
+    exp = analysis.summarize(ref)
+    for k in ("count", "centroid", "rms_radius"):
+        assert np.array_equal(summ[k], exp[k], equal_nan=True), k

@@ -65,3 +65,31 @@ def test_shutdown_then_trace_again():
     assert np.array_equal(after, before, equal_nan=True)
     x = torch.from_numpy(rays).to(DEV)
     assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), before, equal_nan=True)
+
+
+GEN_CASES = {   # tests/golden/make_golden.py: the reference's own generators (RT:45-161) on these arguments
+    "fan": ("fan", ([1., 2., 3.], 0.3, 7, 0.5), dict(nphis=5, center_ray=(0, 0, 1))),
+    "fan_tilted": ("fan", ([0., 0., 0.], 0.2, 5, 0.6), dict(nphis=3, center_ray=tuple(systems.unit([0.6, 0, 0.8])))),
+    "coll": ("coll", ([0., 1., -2.], 3., 5, 0.5), dict(nphis=4, phi_start=0.3)),
+    "coll_tilted": ("coll", ([0., 0., 0.], 2., 4, 0.5), dict(nphis=3, normal=[np.sin(0.2), 0, np.cos(0.2)])),
+    "coll_y": ("coll", ([0., 0., 0.], 2., 3, 0.5), dict(nphis=2, normal=[0, 1, 0])),
+}
+
+
+@pytest.mark.parametrize("name", list(GEN_CASES))
+def test_device_generators_bitwise_vs_reference_fixtures(name):
+    """rtpb_ray_fan_tables / rtpb_collimated_rays_tables (through get_ray_fan / get_collimated_rays with
+    device=) against the reference's own generator output in tests/golden/generators.npz: float64 bit for
+    bit, float32 storage = the fixture rounded once; fans also as per-device phi-row shards."""
+    import os
+    from parity import GOLDEN
+    ref = np.load(os.path.join(GOLDEN, "generators.npz"))[name]
+    kind, args, kw = GEN_CASES[name]
+    gen = rt.get_ray_fan if kind == "fan" else rt.get_collimated_rays
+    got = gen(*args, **kw, device=DEV)
+    assert got.dtype == torch.float64 and np.array_equal(got.cpu().numpy(), ref)
+    got32 = gen(*args, **kw, device=DEV, dtype="float32")
+    assert got32.dtype == torch.float32 and np.array_equal(got32.cpu().numpy(), ref.astype(np.float32))
+    if kind == "fan":
+        shards = gen(*args, **kw, devices=[0, 0, 0])
+        assert np.array_equal(torch.cat([s.cpu() for s in shards]).numpy(), ref)

@@ -1,0 +1,96 @@
+"""BASELINE configs[2] (C3) and configs[3] (C4) at FULL size through the drop-in System.ray_trace.
+
+C3: scripts/2024_08_08_achromat_imaging.py:13-70 -- 5 field points x get_ray_fan(h, 1 deg, 3163, 0.635,
+nphis=3162) = 50,007,030 rays through the 9-surface 4f relay, 19-plane float32 history (30.4 GB).
+C4: scripts/2022_01_25_ray_trace_ideal_opm.py:59-92 -- get_ray_fan(asin(1.35/1.4), 10001, 532e-6,
+nphis=10000) = 100,010,000 rays as 8 per-device shards (all on GPU 0 when only one is visible; the code path
+of 8 GPUs), 23-plane float32 history per shard (73.6 GB in total).
+
+Checked on every ray (size-independent properties): the wavelength column of every plane is the input's
+wavelength or NaN, every finite direction is a unit vector (float32 rounding), the NaN pattern of a row is
+all-or-position-only.  Checked bit for bit: a 20,000-ray random subsample against the NumPy oracle's float64
+history rounded once to float32."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import ray_trace_pb_amd.materials as mat  # noqa: E402
+import ray_trace_pb_amd.raytrace as rt  # noqa: E402
+from oracle import rt_numpy as O  # noqa: E402
+from serialize import material_to_dict, surface_to_dict  # noqa: E402
+import systems  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _oracle_sample(system, m0, m1, rays_dev, hist, n_check, seed):
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(rays_dev.shape[0], n_check, replace=False))
+    it = torch.from_numpy(idx).to(rays_dev.device)
+    ref = O.ray_trace([surface_to_dict(s) for s in system.surfaces],
+                      [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]],
+                      rays_dev.index_select(0, it).cpu().numpy())
+    got = hist.index_select(1, it).cpu().numpy()
+    assert got.dtype == np.float32 and got.shape == ref.shape
+    assert np.array_equal(got, ref.astype(np.float32), equal_nan=True)
+
+
+def _properties(hist, rays_dev):
+    """Every plane: wavelength preserved or NaN; finite directions unit length; positions NaN wherever
+    the direction is NaN (the reference's NaN rules keep d only on sphere misses, never p without d)."""
+    wl = rays_dev[:, 7].float()
+    live_last = None
+    for p in range(hist.shape[0]):
+        h = hist[p]
+        lam = h[:, 7]
+        assert bool(((lam == wl) | torch.isnan(lam)).all()), p
+        d = h[:, 3:6].double()
+        n2 = (d * d).sum(dim=1)
+        fin = torch.isfinite(n2)
+        assert bool(((n2[fin] - 1.0).abs() < 1e-5).all()), p
+        assert bool(torch.isnan(h[~fin, 0]).all()), p
+        live_last = int(torch.isfinite(h[:, 0]).sum())
+    return live_last
+
+
+def test_c3_full_size_float32_history():
+    system, m0, m1 = systems.c3_system(rt, mat), mat.Vacuum(), mat.Vacuum()
+    nt, nph = 3163, 3162
+    per = nt * nph
+    rays = torch.empty((per * len(systems.C3_FIELDS), 8), dtype=torch.float64, device=DEV)
+    for k, h in enumerate(systems.C3_FIELDS):
+        rt.fan_into(rays[k * per:(k + 1) * per], np.array([h, 0, 0]), np.pi / 180, nt, 0.635, nph)
+    assert rays.shape[0] == 50_007_030
+    hist = system.ray_trace(rays, m0, m1, dtype="float32")
+    torch.cuda.synchronize()
+    assert hist.shape == (19, 50_007_030, 8) and hist.dtype == torch.float32
+    assert torch.equal(hist[0], rays.float())
+    live = _properties(hist, rays)
+    assert live > rays.shape[0] // 2
+    _oracle_sample(system, m0, m1, rays, hist, 20_000, 3)
+    del hist, rays
+    torch.cuda.empty_cache()
+
+
+def test_c4_full_size_eight_shards():
+    system, m0, m1 = systems.c4_system(rt, mat), mat.Constant(systems.OPM_N1), mat.Vacuum()
+    theta = 30 * np.pi / 180
+    ndev = torch.cuda.device_count()
+    devs = [k % ndev for k in range(8)]
+    shards = rt.get_ray_fan([1e-3, 1e-3, 1e-3 * np.tan(theta)], np.arcsin(1.35 / systems.OPM_N1), 10001,
+                            systems.OPM_WAVELENGTH, nphis=10000, devices=devs)
+    assert sum(s.shape[0] for s in shards) == 100_010_000
+    hists = system.ray_trace(shards, m0, m1, dtype="float32")
+    for d in set(devs):
+        torch.cuda.synchronize(d)
+    assert len(hists) == 8
+    live = 0
+    for k, (s, h) in enumerate(zip(shards, hists)):
+        assert h.shape == (23, s.shape[0], 8) and h.dtype == torch.float32 and h.device == s.device
+        live += _properties(h, s)
+        _oracle_sample(system, m0, m1, s, h, 2_500, 10 + k)
+    assert live > 0
+    del hists, shards
+    torch.cuda.empty_cache()
