@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4"], help="headline workload")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5"],
+                    help="headline workload (c5: --pmc-child only)")
     ap.add_argument("--configs", default="c2,c4,c5", help="other BASELINE configs in the same line ('none')")
     ap.add_argument("--scale", type=float, default=1.0, help="c3 / c4: fraction of the per-axis fan sizes")
     ap.add_argument("--rays", type=int, default=1_000_000, help="c2: rays per GPU")

@@ -35,10 +35,70 @@ def _f3(v):
     return a
 
 
+_LOWERED = collections.OrderedDict()
+_LOWERED_MAX = 64
+
+
+def _vec_key(v):
+    return np.asarray(v, dtype=np.float64).tobytes()
+
+
+def _lower_key(surfaces, materials, wl, dtype):
+    """Content key of a lowering: every surface / material value lower() reads (the host-side work of
+    lower() is ~0.1-0.2 ms for a 9-surface system -- a few % of a C3 trace -- so repeated traces of the same
+    system reuse the lowered descriptors), or None when some value has no cheap fingerprint."""
+    try:
+        parts = [dtype]
+        for s in surfaces:
+            kind = s._rtpb_kind()
+            p = (kind, _vec_key(s.center), _vec_key(s.input_axis), _vec_key(getattr(s, "normal", s.input_axis)),
+                 float(s.aperture_rad))
+            if kind == C.RTPB_SPHERE:
+                p += (float(s.radius),)
+            elif kind == C.RTPB_PERFECT_LENS:
+                p += (float(s.focal_len), float(s.alpha))
+            parts.append(p)
+        for m in materials:
+            lowered = m._rtpb_lower() if hasattr(m, "_rtpb_lower") else None
+            if lowered is not None:
+                parts.append((lowered[0], tuple(float(c) for c in lowered[1])))
+            else:
+                fp = table_fingerprint([m])
+                if fp is None:
+                    return None
+                parts.append(fp)
+        if wl is not None:
+            parts.append(wl.tobytes())
+        return tuple(parts)
+    except (TypeError, ValueError, AttributeError):
+        return None
+
+
 def lower(surfaces, materials, wavelengths, dtype):
     """Lower surfaces (len S) and materials (len S+1: initial, System.materials, final).
     ``wavelengths`` is a callable returning the distinct wavelengths of the bundle (used only for
-    user Material subclasses, which lower to per-wavelength tables)."""
+    user Material subclasses, which lower to per-wavelength tables).  Results are memoised by content
+    (_lower_key); the Lowered object is read-only once built."""
+    if len(materials) != len(surfaces) + 1:
+        raise ValueError("length of materials should be len(surfaces) + 1")
+    wl = None
+    if tabulated(materials):
+        wl = np.asarray(wavelengths(), dtype=np.float64)
+    key = _lower_key(surfaces, materials, wl, dtype)
+    if key is not None:
+        low = _LOWERED.get(key)
+        if low is not None:
+            _LOWERED.move_to_end(key)
+            return low
+    low = _lower(surfaces, materials, (lambda: wl), dtype)
+    if key is not None:
+        _LOWERED[key] = low
+        while len(_LOWERED) > _LOWERED_MAX:
+            _LOWERED.popitem(last=False)
+    return low
+
+
+def _lower(surfaces, materials, wavelengths, dtype):
     S = len(surfaces)
     if len(materials) != S + 1:
         raise ValueError("length of materials should be len(surfaces) + 1")

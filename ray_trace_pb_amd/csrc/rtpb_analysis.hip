@@ -111,7 +111,8 @@ struct SweepArgs {
     const double* __restrict__ table;
     const double2* __restrict__ tab;    // (cos, sin): thetas [n_thetas], then phis [nphis]
     const double* __restrict__ grp;     // per group: x, y, z, wavelength
-    const double* __restrict__ gn;      // FEAT bit 4: per group, n of the S+1 materials at its wavelength
+    const double* __restrict__ gn;      // FEAT bit 4: per group, n of the S+1 materials at its wavelength, then
+                                        // per surface n_s / n_s+1, 1 / n_s+1 and host_rcp_ok(n_s+1) (0 / 1)
     double* __restrict__ partials;
     int64_t n_thetas, nphis, gsize, tiles;
     double c[3], ex[3], ey[3];
@@ -164,10 +165,10 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
     const cptr<double> table = (cptr<double>)(a.table);
     const double wl0 = r[0].wl;                        // one wavelength per group
-    const Rcp<double> iwl = make_rcp(wl0);             // shared divisor of every phase update
+    const Rcp<double> iwl = make_wl_rcp(wl0);          // shared divisor of every phase update, 2 pi / wl
     // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the
     // kernel's own material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
-    const cptr<double> gn = (cptr<double>)(a.gn) + g * (a.nsurf + 1);
+    const cptr<double> gn = (cptr<double>)(a.gn) + g * (4 * a.nsurf + 1);
     auto mat_n = [&](int k) -> double {
         if constexpr ((FEAT & 16) != 0) return gn[k];
         else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
@@ -175,7 +176,13 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     double n_cur = mat_n(0);
     for (int s = 0; s < a.nsurf; ++s) {
         const double n_next = mat_n(s + 1);
-        const DevSurface<double> sd = load_surface<double>(surf + s);
+        DevSurface<double> sd = load_surface<double>(surf + s);
+        if constexpr ((FEAT & 16) != 0) {
+            // the group's media are uniform: the Snell ratio and 1 / n2 from the host (IEEE division)
+            sd.nr = gn[a.nsurf + 1 + s];
+            sd.rn2 = gn[2 * a.nsurf + 1 + s];
+            sd.rcp_ok = (sd.rcp_ok & 3) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
+        }
         propagate_surface_multi<double, (FEAT & 1) != 0, kSweepRays>(sd, r, n_cur, n_next, iwl);
         n_cur = n_next;
     }
@@ -327,8 +334,10 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     const bool pre_n = (plan->feat & 2) == 0;
     const size_t M = plan->mats.size();
     const size_t ntab = size_t(n_thetas + nphis);
+    const size_t S = static_cast<size_t>(plan->nsurf);
+    const size_t per_group = M + 3 * S;                 // n of every material, then n_s/n_s+1, 1/n_s+1, flags
     const size_t bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) +
-                         (pre_n ? size_t(n_groups) * M * sizeof(double) : 0);
+                         (pre_n ? size_t(n_groups) * per_group * sizeof(double) : 0);
     void* dbuf = nullptr;
     HIP_TRY(hipMallocAsync(&dbuf, bytes, st));
     PinnedStaging& g_pinned = pinned_staging();
@@ -344,8 +353,13 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         for (int64_t gi = 0; gi < n_groups; ++gi) {
             const double w = group_params[4 * gi + 3];
             const double wl = plan->dtype == RTPB_F32 ? double(float(w)) : w;
-            for (size_t k = 0; k < M; ++k)
-                gn[gi * M + k] = material_n<double, false, true>(dm[k], wl, plan->table.data());
+            double* q = gn + gi * per_group;
+            for (size_t k = 0; k < M; ++k) q[k] = material_n<double, false, true>(dm[k], wl, plan->table.data());
+            for (size_t k = 0; k < S; ++k) {
+                q[M + k] = q[k] / q[k + 1];
+                q[M + S + k] = 1.0 / q[k + 1];
+                q[M + 2 * S + k] = host_rcp_ok(q[k + 1]) ? 1.0 : 0.0;
+            }
         }
     }
     rc = g_pinned.upload(dbuf, bytes, st);

@@ -94,7 +94,8 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
     std::vector<unsigned char> blob(p.blob_bytes, 0);
     auto* ds = reinterpret_cast<DevSurface<T>*>(blob.data());
     for (size_t k = 0; k < S; ++k) {
-        const DevSurface<double> d = lower_surface(p.surf[k]);
+        DevSurface<double> d = lower_surface(p.surf[k]);
+        lower_surface_media(d, device_material(p, k), device_material(p, k + 1));
         DevSurface<T>& o = ds[k];
         o.kind = d.kind;
         for (int j = 0; j < 3; ++j) {
@@ -105,6 +106,8 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         o.R = T(d.R); o.R2 = T(d.R2); o.absR = T(d.absR); o.ap = T(d.ap); o.f = T(d.f); o.sin_a = T(d.sin_a);
         o.tol = T(d.tol); o.ap_sq = T(d.ap_sq); o.shell_lo = T(d.shell_lo); o.shell_hi = T(d.shell_hi);
         o.rR = T(d.rR); o.rf = T(d.rf); o.rcp_ok = d.rcp_ok;
+        for (int j = 0; j < 3; ++j) o.nf[j] = T(d.nf[j]);
+        o.nr = T(d.nr); o.rn2 = T(d.rn2);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);

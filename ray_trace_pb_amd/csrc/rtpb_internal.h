@@ -112,6 +112,8 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     d.R = p->R; d.R2 = p->R2; d.absR = p->absR; d.ap = p->ap; d.f = p->f; d.sin_a = p->sin_a; d.tol = p->tol;
     d.ap_sq = p->ap_sq; d.shell_lo = p->shell_lo; d.shell_hi = p->shell_hi;
     d.rR = p->rR; d.rf = p->rf;
+    d.nf[0] = p->nf[0]; d.nf[1] = p->nf[1]; d.nf[2] = p->nf[2];
+    d.nr = p->nr; d.rn2 = p->rn2;
     return d;
 }
 
@@ -289,6 +291,39 @@ __device__ __forceinline__ void tile_flush(const uint4* __restrict__ tile, TS* _
 }
 
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Register-exchange flush of float32 records (no LDS): the same 1 KiB-contiguous stores as tile_flush, with
+// the transpose done by one DPP swap between neighbouring lanes.  It needs the exchange lane mapping:
+// lane 2m traces ray m of the wave's block and lane 2m+1 ray 32+m (xchg_ray).  A record is two 16-byte
+// chunks (lo = x y z dx, hi = dy dz ph wl); store 0 writes chunks 0..63 (rays 0..31), store 1 chunks
+// 64..127 (rays 32..63), so lane 2m stores its own lo and its partner's lo, lane 2m+1 its partner's hi and
+// its own hi: each lane sends one half (even: hi, odd: lo) and receives the other's.
+__device__ __forceinline__ int xchg_ray(int lane) { return (lane & 1) ? 32 + (lane >> 1) : (lane >> 1); }
+
+template <bool NT>
+__device__ __forceinline__ void xchg_flush(float* __restrict__ plane, int64_t ray0, int64_t n, int lane,
+                                           const Ray<double>& r) {
+    constexpr int kAux = NT ? (2 | 16) : 0;            // nt + sc1, as tile_flush
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const float lo[4] = {float(r.x), float(r.y), float(r.z), float(r.dx)};
+    const float hi[4] = {float(r.dy), float(r.dz), float(r.ph), float(r.wl)};
+    const bool odd = (lane & 1) != 0;
+    v4u s0, s1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int send = __float_as_int(odd ? lo[k] : hi[k]);
+        const unsigned recv = static_cast<unsigned>(__builtin_amdgcn_mov_dpp(send, 0xB1, 0xF, 0xF, false));  // lane ^ 1
+        s0[k] = odd ? recv : __float_as_uint(lo[k]);
+        s1[k] = odd ? __float_as_uint(hi[k]) : recv;
+    }
+    const int64_t left = n - ray0;
+    const int nbytes = static_cast<int>((left < 64 ? left : 64) * 32);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(uniform_u64(reinterpret_cast<uint64_t>(plane + ray0 * 8))), static_cast<short>(0),
+        __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(s0, rsrc, lane * 16, 0, kAux);
+    __builtin_amdgcn_raw_buffer_store_b128(s1, rsrc, 1024 + lane * 16, 0, kAux);
+}
 
 // Inverse of tile_flush for the input: lane l loads 16-byte chunks l, l+64, ... of the wave's contiguous
 // record block (1 KiB per load instruction) into the tile, then reads back its own record.

@@ -36,7 +36,8 @@ enum MatKind : int32_t { CONSTANT = 0, SELLMEIER = 1, POLY6 = 2, TABLE = 3,
 template <typename T>
 struct DevSurface {
     int32_t kind;
-    int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok)
+    int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok); bit 2: nr
+                      // and rn2 valid (uniform media); bit 3: rn2 usable by the shared-divisor quotients
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -56,6 +57,14 @@ struct DevSurface {
     // per-lane make_rcp would refine, without its 5 VALU per lane per surface): 1 / radius, 1 / focal_len
     T rR;
     T rf;
+    // PerfectLens: normal * focal_len, the host-side product of F = C - n f n1 and B = C + n f n2 (RT:1682-1687
+    // evaluate `normal * self.focal_len` before the per-ray index)
+    T nf[3];
+    // both adjacent media Constant (rcp_ok bit 2): n1 and n2 are the same for every ray, so the Snell ratio
+    // n1 / n2 (RT:1213) and 1 / n2 (PerfectLens sin_t2, RT:1749) are computed once on the host (IEEE
+    // division: the same correctly rounded values the per-lane divisions give)
+    T nr;
+    T rn2;
 };
 
 template <typename T>
@@ -154,6 +163,13 @@ RTPB_HD void kill(Ray<T>& r) {
     r.x = n; r.y = n; r.z = n; r.dx = n; r.dy = n; r.dz = n; r.ph = n; r.wl = n;
 }
 
+// Per-lane row kill (backward rays, misses, apertures, NA clips); the compiler already branches around the
+// NaN fill (an if-converting variant with a volatile asm barrier measured no faster)
+template <typename T>
+RTPB_HD void kill_if(bool c, Ray<T>& r) {
+    if (c) kill(r);
+}
+
 // NaN-propagating minimum, numpy.minimum / numpy.min semantics
 template <typename T>
 RTPB_HD T nan_min(T a, T b) {
@@ -186,19 +202,19 @@ struct Rcp {
     T b;
     T y;
     bool ok;   // b in the range above (device); host: unused
+    T k;       // make_wl_rcp only: 2 pi / b (the PerfectLens wave number, RT:1773)
 };
 
 #if defined(RTPB_FASTDIV)
+// The range tests read the frexp exponent e (|x| = m 2^e, 0.5 <= m < 1; v_frexp_exp_i32_f64 gives e = 0 for
+// +-0, +-inf and NaN, which are in range either way, and e <= -1021 for denormals, which are not).
 __device__ __forceinline__ bool fastdiv_den_ok(double b) {
-    // biased exponent in [903, 1142]: 2^-120 <= |b| < 2^120 (see fastdiv_num_ok); 0x267: +-0, +-inf, NaN
-    const uint32_t h2 = static_cast<uint32_t>(__double2hiint(b)) << 1;
-    return h2 - (903u << 21) < (240u << 21) || __builtin_amdgcn_class(b, 0x267);
+    // 2^-120 <= |b| < 2^120 <=> -119 <= e <= 120; or b = 0, inf, NaN (e = 0)
+    return static_cast<uint32_t>(__builtin_amdgcn_frexp_exp(b) + 119) <= 239u;
 }
 __device__ __forceinline__ bool fastdiv_num_ok(double a) {
-    // biased exponent in [223, 1622], i.e. 2^-800 <= |a| < 2^600 (a subset of the exact range), on the
-    // high word with 32-bit integer ops: (hi << 1) drops the sign, the subtraction wraps below 223
-    const uint32_t h2 = static_cast<uint32_t>(__double2hiint(a)) << 1;
-    return h2 - (223u << 21) < (1400u << 21) || __builtin_amdgcn_class(a, 0x267);
+    // 2^-800 <= |a| < 2^600 <=> -799 <= e <= 600 (a subset of the exact range); or a = 0, inf, NaN (e = 0)
+    return static_cast<uint32_t>(__builtin_amdgcn_frexp_exp(a) + 799) <= 1399u;
 }
 __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
     const double q0 = a * y;
@@ -212,7 +228,7 @@ __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
 // RN(a/b) when y = RN(1/b)); tests/test_gpu_fastdiv.py checks it on the same adversarial operands
 template <typename T>
 RTPB_HD Rcp<T> host_rcp(T b, T y, bool ok) {
-    return Rcp<T>{b, y, ok};
+    return Rcp<T>{b, y, ok, T(0)};
 }
 
 // host: the range test of fastdiv_den_ok, exactly (2^-120 <= |b| < 2^120, or 0, inf, NaN)
@@ -228,10 +244,10 @@ RTPB_HD Rcp<T> make_rcp(T b) {
         const double y0 = __builtin_amdgcn_rcp(b);
         const double y1 = __builtin_fma(y0, __builtin_fma(-b, y0, 1.0), y0);
         const double y2 = __builtin_fma(y1, __builtin_fma(-b, y1, 1.0), y1);
-        return Rcp<T>{b, y2, fastdiv_den_ok(b)};
+        return Rcp<T>{b, y2, fastdiv_den_ok(b), T(0)};
     }
 #endif
-    return Rcp<T>{b, T(0), true};
+    return Rcp<T>{b, T(0), true, T(0)};
 }
 
 // a / r.b
@@ -271,6 +287,14 @@ RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
 #endif
     (void)g;
     return a / b;
+}
+
+// The per-ray divisor of every phase update (the wavelength) with 2 pi / wl once per ray
+template <typename T, class G = GuardBranch>
+RTPB_HD Rcp<T> make_wl_rcp(T wl, G* g = nullptr) {
+    Rcp<T> r = make_rcp(wl);
+    r.k = div1(T(Const<T>::two_pi), r, g);
+    return r;
 }
 
 // (x, y, z) / r.b, one guard for the three quotients
@@ -379,7 +403,7 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
     o.ph = r.ph + div1_as(dist * s * T(2) * T(Const<T>::pi), r.wl, iwl, g) * n;
     o.wl = r.wl;
-    if (exclude_backward && s == T(-1)) kill(o);
+    kill_if(exclude_backward && s == T(-1), o);
     if (t_out) *t_out = t;
     return o;
 }
@@ -448,11 +472,12 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
 }
 
 // Snell refraction of the intersected ray (RT:1197-1221)
+// ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
 template <typename T, class G = GuardBranch>
-RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T n1, T n2, G* g = nullptr) {
+RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
     T cx, cy, cz;
     tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
-    const T mag = n1 / n2 * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
+    const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
     const T sgn = np_sign<T>(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
     const T tang = sgn * tsqrt<T>(T(1) - mag * mag, g);
     Ray<T> o;
@@ -521,8 +546,8 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
         const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
         emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden, g));   // RT:1790-1793
-        const T Fx = s.c[0] - nx * f * n1, Fy = s.c[1] - ny * f * n1, Fz = s.c[2] - nz * f * n1;
-        const T Bx = s.c[0] + nx * f * n2, By = s.c[1] + ny * f * n2, Bz = s.c[2] + nz * f * n2;
+        const T Fx = s.c[0] - s.nf[0] * n1, Fy = s.c[1] - s.nf[1] * n1, Fz = s.c[2] - s.nf[2] * n1;
+        const T Bx = s.c[0] + s.nf[0] * n2, By = s.c[1] + s.nf[1] * n2, Bz = s.c[2] + s.nf[2] * n2;
         const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
@@ -537,15 +562,17 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         o.x = n1 * f * sin_t1 * spx + Bx;
         o.y = n1 * f * sin_t1 * spy + By;
         o.z = n1 * f * sin_t1 * spz + Bz;
-        const T sin_t2 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g) / n2;
+        const T q1 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
+        const T sin_t2 = (s.rcp_ok & 4) ? div1(q1, host_rcp(n2, s.rn2, (s.rcp_ok & 8) != 0), g) : q1 / n2;
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
         o.dz = sin_t2 * uz + cos_t2 * nz;
         o.wl = r.wl;
-        if (tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a) kill(o);
+        kill_if(tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a, o);
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
-        const T k = div1_as(T(Const<T>::two_pi), r.wl, iwl, g);
+        // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
+        const T k = iwl.k;
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
         after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
                          static_cast<const Rcp<T>*>(nullptr), g);
@@ -566,14 +593,14 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
             after = reflect(ri, Nx, Ny, Nz, g);
-            if (!on_flat(ri, s)) kill(after);
+            kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
-            if (r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0)) kill(ri);
+            kill_if(r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0), ri);
             emit_at(ri);
-            after = snell(ri, Nx, Ny, Nz, n1, n2, g);
+            after = snell(ri, Nx, Ny, Nz, (s.rcp_ok & 4) ? s.nr : n1 / n2, g);
             const bool ok = (KIND == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
-            if (!ok) kill(after);
+            kill_if(!ok, after);
         }
     }
 }
@@ -647,7 +674,7 @@ RTPB_HD void propagate_surface_multi(const DevSurface<T>& s, Ray<T> (&r)[R], T n
 
 template <typename T, bool WITH_LENS = true>
 RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
-    propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, make_rcp(r.wl), [&](const Ray<T>& v) { at = v; }, after);
+    propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, make_wl_rcp(r.wl), [&](const Ray<T>& v) { at = v; }, after);
 }
 
 // ------------------------------------------------------------------ host: descriptor lowering
@@ -721,7 +748,20 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     d.rR = 1.0 / s.radius;                       // IEEE division: RN(1/R) (inf for R = 0)
     d.rf = 1.0 / s.focal_len;
     d.rcp_ok = (host_rcp_ok(s.radius) ? 1 : 0) | (host_rcp_ok(s.focal_len) ? 2 : 0);
+    for (int j = 0; j < 3; ++j) d.nf[j] = s.normal[j] * s.focal_len;     // RT:1682-1687 `normal * focal_len`
+    d.nr = 0.0;
+    d.rn2 = 0.0;
     return d;
+}
+
+// The media on either side (the plan's device materials m1 = before, m2 = after): uniform when both are
+// Constant (MAT:72-79: n does not depend on the wavelength, NaN included).
+inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>& m1, const DevMaterial<double>& m2) {
+    if (m1.kind == CONSTANT && m2.kind == CONSTANT) {
+        d.nr = m1.c[0] / m2.c[0];
+        d.rn2 = 1.0 / m2.c[0];
+        d.rcp_ok |= 4 | (host_rcp_ok(m2.c[0]) ? 8 : 0);
+    }
 }
 
 }  // namespace rtpb

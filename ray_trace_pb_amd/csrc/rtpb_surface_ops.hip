@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kTraceBlock) void interact_kernel(HookArgs a) {
             const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
             const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);
             const double n2 = material_n<double>(load_material<double>(mp + 1), h.wl, a.table);
-            o = snell<double>(h, Nx, Ny, Nz, n1, n2);                               // RT:1194-1221
+            o = snell<double>(h, Nx, Ny, Nz, n1 / n2);                              // RT:1194-1221
         }
         if (a.on && !a.on[i]) kill(o);                                               // RT:1225-1226, 1293-1294
         tile_write<TS>(tile, lane, o);

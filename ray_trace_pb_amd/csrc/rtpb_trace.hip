@@ -334,7 +334,8 @@ int rtpb_trace_host(const rtpb_plan* plan_c, const void* rays_in, int32_t in_dty
 int rtpb_set_tuning(const char* key, int64_t value) {
     if (!key) return fail(RTPB_E_INVALID, "key is NULL");
     if (std::strcmp(key, "aos_staging") == 0) {
-        g_aos_staging.store(value != 0);
+        if (value < 0 || value > 2) return fail(RTPB_E_INVALID, "aos_staging must be 0, 1 or 2");
+        g_aos_staging.store(static_cast<int>(value));
         return RTPB_OK;
     }
     if (std::strcmp(key, "nt_stores") == 0) {

@@ -57,6 +57,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     using T = double;
     constexpr bool kStaged = (STORE & 1) && OUT_LAYOUT == RTPB_AOS;
     constexpr bool kNT = (STORE & 2) != 0;
+    // STORE bit 4: float32 records flushed by a register exchange instead of the LDS tiles (xchg_flush)
+    constexpr bool kXchg = (STORE & 16) != 0;
+    static_assert(!kXchg || (kStaged && sizeof(TS) == 4 && kB == 64), "exchange flush: staged float32 AOS");
     // STORE bit 3: only the final plane is stored (planes='final'): no per-surface store logic, one
     // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
     constexpr bool kFinal = (STORE & 8) != 0;
@@ -78,8 +81,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     // one block of kB rays per workgroup (blocks go round-robin over the XCDs: measured faster than
     // XCD-contiguous block ranges).  The body is a lambda of the block index; called once.
     auto body = [&](const int64_t blk) {
-    const int64_t i = blk * kB + threadIdx.x;
-    const int64_t ray0 = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(i - lane)));  // first ray of this wave
+    const int64_t i = kXchg ? blk * kB + xchg_ray(lane) : blk * kB + threadIdx.x;
+    const int64_t ray0 = kXchg ? blk * kB
+                               : static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(i - lane)));  // first ray of this wave
     if (ray0 >= a.n) return;                             // wave-uniform exit
     const bool valid = i < a.n;
     uint4* tile_a = tiles[threadIdx.x >> 6][0];
@@ -90,7 +94,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         r = tile_load<TS>(tile_b, a.in, ray0, a.n, lane);
     else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);
     const T wl0 = r.wl;
-    const Rcp<T> iwl = make_rcp(wl0);                    // shared divisor of every phase update
+    const Rcp<T> iwl = make_wl_rcp(wl0);                 // shared divisor of every phase update, 2 pi / wl
     TS* __restrict__ out = a.out;
     const cptr<DevSurface<T>> surf = (cptr<DevSurface<T>>)(a.surf);
     const cptr<DevMaterial<T>> mats = (cptr<DevMaterial<T>>)(a.mats);
@@ -136,7 +140,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             r = after;
             n_cur = n_next;
         }
-        if constexpr (kStaged) {
+        if constexpr (kXchg) {
+            xchg_flush<kNT>(out, ray0, a.n, lane, r);
+        } else if constexpr (kStaged) {
             tile_write<TS>(tile_b, lane, r);
             lds_wait();
             tile_flush<TS, kNT>(tile_b, out, ray0, a.n, lane);
@@ -147,7 +153,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     }
     int64_t slot_off = 0;
     if (a.mask_lo & 1ull) {
-        if constexpr (kStaged) {
+        if constexpr (kXchg) {
+            xchg_flush<kNT>(out, ray0, a.n, lane, r);
+        } else if constexpr (kStaged) {
             tile_write<TS>(tile_a, lane, r);
             lds_wait();
             tile_flush<TS, kNT>(tile_a, out, ray0, a.n, lane);
@@ -168,7 +176,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         slot_off += st_after ? a.out_ps : 0;
         // the "at" plane goes to its LDS tile (or straight out) as soon as it is final
         auto emit_at = [&](const Ray<T>& at) {
-            if constexpr (kStaged) {
+            if constexpr (kXchg) {
+                if (st_at) xchg_flush<kNT>(out + off_at, ray0, a.n, lane, at);
+            } else if constexpr (kStaged) {
                 if (st_at) tile_write<TS>(tile_a, lane, at);
             } else {
                 if (valid && st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
@@ -176,7 +186,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         };
         Ray<T> after;
         propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
-        if constexpr (kStaged) {
+        if constexpr (kXchg) {
+            if (st_after) xchg_flush<kNT>(out + off_after, ray0, a.n, lane, after);
+        } else if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
             if (st_after) tile_write<TS>(tile_b, lane, after);
             if (st_at || st_after) lds_wait();
@@ -226,23 +238,38 @@ hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
 
 template <typename TI, typename T>
 hipError_t launch_trace(const TraceArgs<TI, T>& a, int il, int ol, int feat, hipStream_t st) {
-    const bool staged = g_aos_staging.load() != 0;
+    const int staging = g_aos_staging.load();
+    const bool staged = staging != 0;
     const bool nt = g_nt_stores.load() != 0;
+    // aos_staging 2: float32 storage flushed by register exchange (STORE bit 4) instead of LDS tiles
+    constexpr bool kF32 = sizeof(T) == 4;
+    const bool xchg = kF32 && staging == 2 && nt;
     const int last = 2 * a.nsurf;                       // planes='final': only the last plane stored
     const bool final_only = a.nsurf > 0 && (last < 64 ? (a.mask_lo == (1ull << last) && a.mask_hi == 0)
                                                       : (a.mask_lo == 0 && a.mask_hi == (1ull << (last - 64))));
     if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load())
+    {
+        if constexpr (kF32) {
+            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 27>(a, feat, st);
+        }
         return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 11>(a, feat, st);
+    }
     if constexpr (!std::is_same<TI, T>::value) {
         // input and storage types differ: AOS input only (rtpb_trace checks), no staged-input variant
         if (ol == RTPB_SOA) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
         if (!staged) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st);
+        if constexpr (kF32) {
+            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19>(a, feat, st);
+        }
         return nt ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st);
     }
     if (ol == RTPB_AOS) {
         if (!staged)
             return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 0>(a, feat, st);
         if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 7>(a, feat, st);
+        if constexpr (kF32) {
+            if (xchg && il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19>(a, feat, st);
+        }
         if (nt)
             return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 3>(a, feat, st);
         return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 1>(a, feat, st);

@@ -942,6 +942,26 @@ class Doublet(System):
 
 
 # =============================================================================== surfaces
+_SURFACE_CLASS_INFO = {}
+
+
+def _surface_class_info(cls):
+    """(own propagate, own geometry hooks, fused-kernel kind class or None) of a Surface class -- class
+    properties, computed once per class (they are queried on every trace)."""
+    info = _SURFACE_CLASS_INFO.get(cls)
+    if info is None:
+        owner = cls._rtpb_owner
+        user_prop = owner("propagate").__module__ != __name__
+        kind_cls = next((c for c in cls.__mro__ if "_RTPB_KIND" in c.__dict__ and c._RTPB_KIND is not None), None)
+        if user_prop or not issubclass(cls, (RefractingSurface, ReflectingSurface)) or kind_cls is PerfectLens:
+            user_geom = False
+        else:
+            user_geom = kind_cls is None or any(owner(m).__module__ != __name__ for m in Surface._GEOMETRY[1:])
+        info = (user_prop, user_geom, kind_cls)
+        _SURFACE_CLASS_INFO[cls] = info
+    return info
+
+
 class Surface:
     """Base optical surface: input/output axes, center, paraxial center, aperture radius (RT:1031-1156)."""
 
@@ -957,7 +977,7 @@ class Surface:
     _GEOMETRY = ("propagate", "get_intersect", "get_normal", "is_pt_on_surface")
 
     def _rtpb_kind_class(self):
-        return next((c for c in type(self).__mro__ if "_RTPB_KIND" in c.__dict__ and c._RTPB_KIND is not None), None)
+        return _surface_class_info(type(self))[2]
 
     @classmethod
     def _rtpb_owner(cls, name):
@@ -966,19 +986,14 @@ class Surface:
     def _rtpb_user_propagate(self):
         """True for a user subclass that supplies its own ``propagate`` (the reference's plugin point,
         RT:1092-1104, as PerfectLens does): System.ray_trace then runs that code for this surface."""
-        return self._rtpb_owner("propagate").__module__ != __name__
+        return _surface_class_info(type(self))[0]
 
     def _rtpb_user_geometry(self):
         """True for a user RefractingSurface / ReflectingSurface subclass that keeps the base propagate
         but supplies its own get_intersect / get_normal / is_pt_on_surface (RT:1071-1156): traced by
         propagate_user_geometry (user hooks + GPU Snell/reflection).  PerfectLens subclasses keep the
         lens kernel: PerfectLens.propagate never calls the hooks (RT:1680-1801)."""
-        if self._rtpb_user_propagate() or not isinstance(self, (RefractingSurface, ReflectingSurface)):
-            return False
-        kind_cls = self._rtpb_kind_class()
-        if kind_cls is PerfectLens:
-            return False
-        return kind_cls is None or any(self._rtpb_owner(m).__module__ != __name__ for m in self._GEOMETRY[1:])
+        return _surface_class_info(type(self))[1]
 
     def _rtpb_kind(self):
         kind_cls = self._rtpb_kind_class()

@@ -35,6 +35,7 @@ static int harness_trace(const rtpb_surface* surfaces, int32_t nsurf, const rtpb
             sort_table(table.data() + table.size() - 2 * m.table_len, m.table_len);
         }
     }
+    for (int k = 0; k < nsurf; ++k) lower_surface_media(S[k], M[k], M[k + 1]);
     const int64_t P = 2 * nsurf + 1;
     for (int64_t i = 0; i < n; ++i) {
         const TS* a = in + 8 * i;

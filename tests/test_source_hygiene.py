@@ -1,13 +1,8 @@
-"""The shipped kernel sources carry no experiment switches; the experiments live in
-tools/experiments/experiments.patch (applied by tools/exp_build.py to a scratch copy) and that patch must
-keep applying to the current sources."""
+"""The shipped kernel sources carry no experiment switches: experiments are source edits applied to a
+scratch copy (tools/exp_variants.py, tools/exp_build.py); the round-2 switches are kept as a patch against
+the round-2 sources (profiles/r02/experiments/experiments_round2.patch)."""
 import glob
 import os
-import shutil
-import subprocess
-import tempfile
-
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "ray_trace_pb_amd", "csrc")
@@ -20,13 +15,3 @@ def test_no_experiment_switches_in_shipped_sources():
             if "RTPB_EXP_" in line or "RTPB_FLOAT_RANGE_CHECKS" in line:
                 hits.append(f"{os.path.basename(p)}:{k}")
     assert not hits, hits
-
-
-@pytest.mark.skipif(not shutil.which("patch"), reason="patch(1) not available")
-def test_experiments_patch_applies():
-    with tempfile.TemporaryDirectory() as tmp:
-        shutil.copytree(CSRC, os.path.join(tmp, "ray_trace_pb_amd", "csrc"), ignore=shutil.ignore_patterns("_obj"))
-        r = subprocess.run(["patch", "-p1", "--dry-run", "-d", tmp, "-i",
-                            os.path.join(ROOT, "tools", "experiments", "experiments.patch")],
-                           capture_output=True, text=True)
-        assert r.returncode == 0, r.stdout + r.stderr

@@ -29,8 +29,9 @@ import systems  # noqa: E402
 def load(path):
     h = ctypes.CDLL(os.path.abspath(path))          # RTLD_LOCAL: each build keeps its own symbols/kernels
     for name, (res, argt) in C.SIGNATURES.items():
-        fn = getattr(h, name)
-        fn.restype, fn.argtypes = res, argt
+        fn = getattr(h, name, None)          # an older build may lack newer entry points
+        if fn is not None:
+            fn.restype, fn.argtypes = res, argt
     return h
 
 

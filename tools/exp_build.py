@@ -1,12 +1,11 @@
-"""Build an EXPERIMENT variant of librtpb.so: the shipped sources carry no experiment branches, so this
-copies ray_trace_pb_amd/csrc to a scratch directory, applies tools/experiments/experiments.patch (which
-restores the RTPB_EXP_* switches: NO_COMPUTE, NO_GUARDS, NO_MATERIAL, NO_ONSURFACE, NO_INPUT, XCD_REMAP,
-SCATTER, STAGGER, FLUSH_SYNC, PERSIST, MAXW, WPE, STORE_AUX, TRACE_BLOCK, FLOAT_RANGE_CHECKS, the
-waves_per_eu=5 knob) and any extra patches, and compiles with the given -D flags.  Never shipped: used by
-tools/ab_variants.py / tools/ab_libs.py to find where kernel time goes.
+"""Build an EXPERIMENT variant of librtpb.so from a patched scratch copy of the sources: the shipped
+sources carry no experiment branches.  Applies the given patches (-p1, repository-relative paths) and
+compiles with the given -D flags.  Never shipped: used by tools/ab_variants.py / tools/ab_libs.py to find
+where kernel time goes.  Named variants with reviewable source edits: tools/exp_variants.py.  The round-2
+switches (RTPB_EXP_NO_COMPUTE, XCD_REMAP, PERSIST, ...) are profiles/r02/experiments/experiments_round2.patch,
+which applies to the round-2 sources (commit 7b1cac3).
 
-    python tools/exp_build.py --out ray_trace_pb_amd/exp_nocomp.so -DRTPB_EXP_NO_COMPUTE
-    python tools/exp_build.py --out ray_trace_pb_amd/exp_x.so --patch my.patch --no-exp-patch
+    python tools/exp_build.py --out ray_trace_pb_amd/exp_x.so --patch my.patch -DMY_SWITCH
 """
 import argparse
 import os
@@ -19,14 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from ray_trace_pb_amd import _build  # noqa: E402
 
-EXP_PATCH = os.path.join(ROOT, "tools", "experiments", "experiments.patch")
 
-
-def build(out, flags=(), patches=(), exp_patch=True):
+def build(out, flags=(), patches=()):
     with tempfile.TemporaryDirectory() as tmp:
         shutil.copytree(_build.CSRC, os.path.join(tmp, "ray_trace_pb_amd", "csrc"),
                         ignore=shutil.ignore_patterns("_obj"))
-        for p in ([EXP_PATCH] if exp_patch else []) + list(patches):
+        for p in patches:
             subprocess.run(["patch", "-p1", "-s", "-d", tmp, "-i", os.path.abspath(p)], check=True)
         return _build.build(force=True, verbose=False, extra_flags=list(flags), out=os.path.abspath(out),
                             csrc=os.path.join(tmp, "ray_trace_pb_amd", "csrc"))
@@ -36,9 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--patch", action="append", default=[])
-    ap.add_argument("--no-exp-patch", action="store_true")
     args, flags = ap.parse_known_args()
-    print(build(args.out, flags, args.patch, not args.no_exp_patch))
+    print(build(args.out, flags, args.patch))
 
 
 if __name__ == "__main__":
