@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
             // the group's media are uniform: the Snell ratio and 1 / n2 from the host (IEEE division)
             sd.nr = gn[a.nsurf + 1 + s];
             sd.rn2 = gn[2 * a.nsurf + 1 + s];
-            sd.rcp_ok = (sd.rcp_ok & 3) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
+            sd.rcp_ok = (sd.rcp_ok & ~(4 | 8)) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
         }
         propagate_surface_multi<double, (FEAT & 1) != 0, kSweepRays>(sd, r, n_cur, n_next, iwl);
         n_cur = n_next;

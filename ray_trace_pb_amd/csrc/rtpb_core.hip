@@ -49,7 +49,8 @@ DevMaterial<double> device_material(const rtpb_plan& p, size_t k) {
 // Indexed materials (kLdsIndexedDoubles): when every TABLE material shares one strictly increasing key
 // set (NaN last allowed) and there is no POLY6 material, tabulate every material at those keys --
 // TABLE materials by their own values, the others with material_n itself (host build of the kernel's
-// function, -ffp-contract=off: the same IEEE operations, hence the same bits).
+// function, -ffp-contract=off: the same IEEE operations, hence the same bits) -- and every surface's Snell
+// ratio n_s / n_s+1 at those keys.
 void build_indexed(rtpb_plan& p) {
     if (p.table.empty() || (p.feat & 2)) return;
     const size_t M = p.mats.size();
@@ -58,7 +59,8 @@ void build_indexed(rtpb_plan& p) {
         if (p.mats[k].kind == RTPB_TABLE) { first = static_cast<int>(k); break; }
     if (first < 0) return;
     const int K = p.mats[first].table_len;
-    if (K <= 0 || static_cast<size_t>(K) * (M + 1) > static_cast<size_t>(kLdsIndexedDoubles)) return;
+    const size_t S = p.surf.size();
+    if (K <= 0 || static_cast<size_t>(K) * (M + 1 + S) > static_cast<size_t>(kLdsIndexedDoubles)) return;
     const double* keys0 = p.table.data() + 2 * static_cast<size_t>(p.table_off[first]);
     for (int j = 0; j < K; ++j) {
         const double kj = keys0[2 * j];
@@ -74,7 +76,7 @@ void build_indexed(rtpb_plan& p) {
             if (a != a ? b == b : std::memcmp(&a, &b, sizeof(double)) != 0) return;
         }
     }
-    std::vector<double> it(static_cast<size_t>(K) * (M + 1));
+    std::vector<double> it(static_cast<size_t>(K) * (M + 1 + S));
     for (int j = 0; j < K; ++j) it[j] = keys0[2 * j];
     for (size_t k = 0; k < M; ++k) {
         const double* kk = p.table.data() + 2 * static_cast<size_t>(p.table_off[k]);
@@ -83,6 +85,9 @@ void build_indexed(rtpb_plan& p) {
             it[K * (k + 1) + j] = p.mats[k].kind == RTPB_TABLE ? kk[2 * j + 1]
                                                                : material_n<double, false, false>(d, keys0[2 * j], static_cast<const double*>(nullptr));
     }
+    // the Snell ratio n_s / n_s+1 of every surface at every key (IEEE division: the per-lane quotient)
+    for (size_t s = 0; s < S; ++s)
+        for (int j = 0; j < K; ++j) it[K * (M + 1 + s) + j] = it[K * (s + 1) + j] / it[K * (s + 2) + j];
     p.itab.swap(it);
     p.nkeys = K;
     p.feat = (p.feat & ~(4 | 8)) | 16;
@@ -108,6 +113,11 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         o.rR = T(d.rR); o.rf = T(d.rf); o.rcp_ok = d.rcp_ok;
         for (int j = 0; j < 3; ++j) o.nf[j] = T(d.nf[j]);
         o.nr = T(d.nr); o.rn2 = T(d.rn2);
+        for (int j = 0; j < 3; ++j) {
+            o.F[j] = T(d.F[j]);
+            o.B[j] = T(d.B[j]);
+        }
+        o.n1f = T(d.n1f); o.nnf = T(d.nnf);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);

@@ -70,7 +70,7 @@ struct TraceArgs {
     const DevSurface<double>* __restrict__ surf;
     const DevMaterial<double>* __restrict__ mats;
     const double* __restrict__ table;
-    const double* __restrict__ itab;   // indexed materials: [nkeys keys][(nsurf+1) x nkeys values]
+    const double* __restrict__ itab;   // indexed materials: [nkeys keys][(nsurf+1) x nkeys n][nsurf x nkeys ratios]
     int32_t* miss;        // rtpb_trace_checked: set to 1 when a ray's wavelength is no TABLE key (or NULL)
     int64_t n;
     int64_t in_fs;        // SOA input field stride
@@ -114,6 +114,11 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     d.rR = p->rR; d.rf = p->rf;
     d.nf[0] = p->nf[0]; d.nf[1] = p->nf[1]; d.nf[2] = p->nf[2];
     d.nr = p->nr; d.rn2 = p->rn2;
+    for (int j = 0; j < 3; ++j) {
+        d.F[j] = p->F[j];
+        d.B[j] = p->B[j];
+    }
+    d.n1f = p->n1f; d.nnf = p->nnf;
     return d;
 }
 
@@ -207,7 +212,8 @@ constexpr int kLdsTablePairs = 256;
 // with the kernel's own material_n (so the values are the ones the kernel would compute).  The kernel
 // then finds each ray's key index once and reads n(material, key) from LDS at every surface, instead of
 // re-evaluating Sellmeier dispersion (three divisions and a square root) and searching tables per
-// surface.  Layout: [K keys][(S+1) x K values]; at most this many doubles.
+// surface, and each surface's Snell ratio n1 / n2 instead of dividing.  Layout: [K keys][(S+1) x K
+// values][S x K ratios]; at most this many doubles.
 constexpr int kLdsIndexedDoubles = 512;
 
 // Index of wavelength wl among the K sorted keys (NaN last, as sort_table orders them; NaN wl finds a NaN
@@ -408,7 +414,7 @@ struct rtpb_plan {
     // the kernel's LDS copy (kLdsTablePairs), 8 = TABLE materials read from global memory, 16 = indexed
     // materials (replaces 4 / 8; see kLdsIndexedDoubles)
     int feat = 0;
-    std::vector<double> itab;           // indexed materials: [nkeys keys][(nsurf+1) x nkeys values]
+    std::vector<double> itab;           // indexed materials: [nkeys keys][(nsurf+1) x nkeys n][nsurf x nkeys ratios]
     int32_t nkeys = 0;
     std::mutex mu;
     void* blob[rtpbi::kMaxDevices] = {};

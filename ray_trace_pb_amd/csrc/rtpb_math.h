@@ -37,7 +37,8 @@ template <typename T>
 struct DevSurface {
     int32_t kind;
     int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok); bit 2: nr
-                      // and rn2 valid (uniform media); bit 3: rn2 usable by the shared-divisor quotients
+                      // valid; bit 3: rn2 valid and usable by the quotients; bit 4: the PerfectLens constants
+                      // of uniform media (F, B, n1f, nnf) valid
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -65,6 +66,12 @@ struct DevSurface {
     // division: the same correctly rounded values the per-lane divisions give)
     T nr;
     T rn2;
+    // PerfectLens between uniform media: the front / back focal points F = C - n f n1, B = C + n f n2
+    // (RT:1682-1687), n1 f (RT:1743) and n1^2 f + n2^2 f (RT:1775), all as the per-ray code evaluates them
+    T F[3];
+    T B[3];
+    T n1f;
+    T nnf;
 };
 
 template <typename T>
@@ -401,7 +408,9 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     o.z = r.z + vz;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
-    o.ph = r.ph + div1_as(dist * s * T(2) * T(Const<T>::pi), r.wl, iwl, g) * n;
+    // dist * s * 2 * pi (RT:297): s = +-1 is a sign, and 2 * pi is exact, so ((d s) 2) pi == (+-d) (2 pi)
+    // bit for bit -- the two real products are the same number (overflow to inf included)
+    o.ph = r.ph + div1_as((s < T(0) ? -dist : dist) * T(Const<T>::two_pi), r.wl, iwl, g) * n;
     o.wl = r.wl;
     kill_if(exclude_backward && s == T(-1), o);
     if (t_out) *t_out = t;
@@ -429,7 +438,7 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
     const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz, g);
-    o.ph = r.ph + div1_as(dist * T(2) * T(Const<T>::pi), r.wl, iwl, g) * n;
+    o.ph = r.ph + div1_as(dist * T(Const<T>::two_pi), r.wl, iwl, g) * n;     // == (d 2) pi, see to_plane
     o.wl = r.wl;
     return o;
 }
@@ -546,8 +555,11 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
         const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
         emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden, g));   // RT:1790-1793
-        const T Fx = s.c[0] - s.nf[0] * n1, Fy = s.c[1] - s.nf[1] * n1, Fz = s.c[2] - s.nf[2] * n1;
-        const T Bx = s.c[0] + s.nf[0] * n2, By = s.c[1] + s.nf[1] * n2, Bz = s.c[2] + s.nf[2] * n2;
+        const bool uni = (s.rcp_ok & 16) != 0;             // uniform media: host-side constants
+        const T Fx = uni ? s.F[0] : s.c[0] - s.nf[0] * n1, Fy = uni ? s.F[1] : s.c[1] - s.nf[1] * n1,
+                Fz = uni ? s.F[2] : s.c[2] - s.nf[2] * n1;
+        const T Bx = uni ? s.B[0] : s.c[0] + s.nf[0] * n2, By = uni ? s.B[1] : s.c[1] + s.nf[1] * n2,
+                Bz = uni ? s.B[2] : s.c[2] + s.nf[2] * n2;
         const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
@@ -559,11 +571,12 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n), g);
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
-        o.x = n1 * f * sin_t1 * spx + Bx;
-        o.y = n1 * f * sin_t1 * spy + By;
-        o.z = n1 * f * sin_t1 * spz + Bz;
+        const T h = (uni ? s.n1f : n1 * f) * sin_t1;
+        o.x = h * spx + Bx;
+        o.y = h * spy + By;
+        o.z = h * spz + Bz;
         const T q1 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
-        const T sin_t2 = (s.rcp_ok & 4) ? div1(q1, host_rcp(n2, s.rn2, (s.rcp_ok & 8) != 0), g) : q1 / n2;
+        const T sin_t2 = (s.rcp_ok & 8) ? div1(q1, host_rcp(n2, s.rn2, true), g) : q1 / n2;
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
@@ -573,7 +586,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
         // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
         const T k = iwl.k;
-        o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
+        o.ph = rf.ph - k * n1 * pw + k * (uni ? s.nnf : n1 * n1 * f + n2 * n2 * f);
         after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
                          static_cast<const Rcp<T>*>(nullptr), g);
     } else {
@@ -751,6 +764,8 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     for (int j = 0; j < 3; ++j) d.nf[j] = s.normal[j] * s.focal_len;     // RT:1682-1687 `normal * focal_len`
     d.nr = 0.0;
     d.rn2 = 0.0;
+    for (int j = 0; j < 3; ++j) d.F[j] = d.B[j] = 0.0;
+    d.n1f = d.nnf = 0.0;
     return d;
 }
 
@@ -758,9 +773,19 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
 // Constant (MAT:72-79: n does not depend on the wavelength, NaN included).
 inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>& m1, const DevMaterial<double>& m2) {
     if (m1.kind == CONSTANT && m2.kind == CONSTANT) {
-        d.nr = m1.c[0] / m2.c[0];
-        d.rn2 = 1.0 / m2.c[0];
-        d.rcp_ok |= 4 | (host_rcp_ok(m2.c[0]) ? 8 : 0);
+        const double n1 = m1.c[0], n2 = m2.c[0], f = d.f;
+        d.nr = n1 / n2;
+        d.rn2 = 1.0 / n2;
+        d.rcp_ok |= 4 | (host_rcp_ok(n2) ? 8 : 0);
+        if (d.kind == PERFECT_LENS) {            // the per-ray expressions of surface_step, evaluated once
+            for (int j = 0; j < 3; ++j) {
+                d.F[j] = d.c[j] - d.nf[j] * n1;
+                d.B[j] = d.c[j] + d.nf[j] * n2;
+            }
+            d.n1f = n1 * f;
+            d.nnf = n1 * n1 * f + n2 * n2 * f;
+            d.rcp_ok |= 16;
+        }
     }
 }
 

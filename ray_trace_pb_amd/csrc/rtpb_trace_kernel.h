@@ -69,7 +69,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
                                                          // FEAT bit 4: the indexed-material table
     if constexpr (kTabLds || kIdx) {
         // before any wave can leave: the unstaged variants run four-wave workgroups and need the barrier
-        const int cnt = kIdx ? a.nkeys * (a.nsurf + 2) : 2 * a.ntable;
+        const int cnt = kIdx ? a.nkeys * (2 * a.nsurf + 2) : 2 * a.ntable;
         const double* src = kIdx ? a.itab : a.table;
         for (int k = threadIdx.x; k < cnt; k += kB) lds_table[k] = src[k];
         if constexpr (kB > 64) __syncthreads();
@@ -120,6 +120,18 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             if (valid && miss) a.miss[0] = 1;
         }
     }
+    // every lane of the wave has its key: the surfaces' Snell ratios come from the table too (uniform test)
+    const bool all_idx = kIdx && __builtin_amdgcn_ballot_w64(widx < 0) == 0;
+    auto surface = [&](int s) -> DevSurface<T> {
+        DevSurface<T> d = load_surface<T>(surf + s);
+        if constexpr (kIdx) {
+            if (all_idx && !(d.rcp_ok & 4)) {
+                d.nr = lds_table[a.nkeys * (a.nsurf + 2 + s) + widx];
+                d.rcp_ok |= 4;
+            }
+        }
+        return d;
+    };
     auto mat_n = [&](cptr<DevMaterial<T>> mp) -> T {
         if constexpr (kIdx) {
             if (widx >= 0) return lds_table[a.nkeys * (1 + static_cast<int>(mp - mats)) + widx];
@@ -135,7 +147,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         for (int s = 0; s < a.nsurf; ++s) {
             const T n_next = mat_n(mats + s + 1);
             Ray<T> after;
-            propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl,
+            propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_next, iwl,
                                              [](const Ray<T>&) {}, after);
             r = after;
             n_cur = n_next;
@@ -185,7 +197,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
             }
         };
         Ray<T> after;
-        propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);
+        propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_next, iwl, emit_at, after);
         if constexpr (kXchg) {
             if (st_after) xchg_flush<kNT>(out + off_after, ray0, a.n, lane, after);
         } else if constexpr (kStaged) {
@@ -210,7 +222,7 @@ template <typename TI, typename T, int IL, int OL, int ST, int W, int FEAT>
 hipError_t launch_w(const TraceArgs<TI, T>& a, hipStream_t st) {
     constexpr int kB = trace_block(OL, ST);
     const int64_t blocks = (a.n + kB - 1) / kB;
-    const size_t lds = (FEAT & 16)        ? static_cast<size_t>(a.nkeys) * (a.nsurf + 2) * sizeof(double)
+    const size_t lds = (FEAT & 16)        ? static_cast<size_t>(a.nkeys) * (2 * a.nsurf + 2) * sizeof(double)
                        : (FEAT & 12) == 4 ? static_cast<size_t>(a.ntable) * 2 * sizeof(double) : 0;
     hipLaunchKernelGGL((trace_kernel<TI, T, IL, OL, ST, W, FEAT>), dim3(static_cast<unsigned>(blocks)), dim3(kB), lds,
                        st, a);
