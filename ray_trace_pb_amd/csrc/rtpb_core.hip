@@ -113,11 +113,6 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         o.rR = T(d.rR); o.rf = T(d.rf); o.rcp_ok = d.rcp_ok;
         for (int j = 0; j < 3; ++j) o.nf[j] = T(d.nf[j]);
         o.nr = T(d.nr); o.rn2 = T(d.rn2);
-        for (int j = 0; j < 3; ++j) {
-            o.F[j] = T(d.F[j]);
-            o.B[j] = T(d.B[j]);
-        }
-        o.n1f = T(d.n1f); o.nnf = T(d.nnf);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);

@@ -114,11 +114,6 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     d.rR = p->rR; d.rf = p->rf;
     d.nf[0] = p->nf[0]; d.nf[1] = p->nf[1]; d.nf[2] = p->nf[2];
     d.nr = p->nr; d.rn2 = p->rn2;
-    for (int j = 0; j < 3; ++j) {
-        d.F[j] = p->F[j];
-        d.B[j] = p->B[j];
-    }
-    d.n1f = p->n1f; d.nnf = p->nnf;
     return d;
 }
 

@@ -37,8 +37,7 @@ template <typename T>
 struct DevSurface {
     int32_t kind;
     int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok); bit 2: nr
-                      // valid; bit 3: rn2 valid and usable by the quotients; bit 4: the PerfectLens constants
-                      // of uniform media (F, B, n1f, nnf) valid
+                      // valid; bit 3: rn2 valid and usable by the quotients
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -66,12 +65,6 @@ struct DevSurface {
     // division: the same correctly rounded values the per-lane divisions give)
     T nr;
     T rn2;
-    // PerfectLens between uniform media: the front / back focal points F = C - n f n1, B = C + n f n2
-    // (RT:1682-1687), n1 f (RT:1743) and n1^2 f + n2^2 f (RT:1775), all as the per-ray code evaluates them
-    T F[3];
-    T B[3];
-    T n1f;
-    T nnf;
 };
 
 template <typename T>
@@ -176,6 +169,14 @@ template <typename T>
 RTPB_HD void kill_if(bool c, Ray<T>& r) {
     if (c) kill(r);
 }
+
+// Selects a value by a wave-uniform descriptor bit as a real (scalar) branch: the empty volatile asm keeps
+// the compiler from speculating the per-lane computation into a select, which would run it on every path.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTPB_NO_SPECULATE() asm volatile("")
+#else
+#define RTPB_NO_SPECULATE() ((void)0)
+#endif
 
 // NaN-propagating minimum, numpy.minimum / numpy.min semantics
 template <typename T>
@@ -555,11 +556,10 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
         const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
         emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden, g));   // RT:1790-1793
-        const bool uni = (s.rcp_ok & 16) != 0;             // uniform media: host-side constants
-        const T Fx = uni ? s.F[0] : s.c[0] - s.nf[0] * n1, Fy = uni ? s.F[1] : s.c[1] - s.nf[1] * n1,
-                Fz = uni ? s.F[2] : s.c[2] - s.nf[2] * n1;
-        const T Bx = uni ? s.B[0] : s.c[0] + s.nf[0] * n2, By = uni ? s.B[1] : s.c[1] + s.nf[1] * n2,
-                Bz = uni ? s.B[2] : s.c[2] + s.nf[2] * n2;
+        // (host-side F, B and n^2 f for uniform media measured 3 % slower on C4: the merged values cost
+        // registers, profiles/r03/experiments/ab_lens_constants.log)
+        const T Fx = s.c[0] - s.nf[0] * n1, Fy = s.c[1] - s.nf[1] * n1, Fz = s.c[2] - s.nf[2] * n1;
+        const T Bx = s.c[0] + s.nf[0] * n2, By = s.c[1] + s.nf[1] * n2, Bz = s.c[2] + s.nf[2] * n2;
         const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
@@ -571,12 +571,18 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n), g);
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
-        const T h = (uni ? s.n1f : n1 * f) * sin_t1;
+        const T h = n1 * f * sin_t1;
         o.x = h * spx + Bx;
         o.y = h * spy + By;
         o.z = h * spz + Bz;
         const T q1 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
-        const T sin_t2 = (s.rcp_ok & 8) ? div1(q1, host_rcp(n2, s.rn2, true), g) : q1 / n2;
+        T sin_t2;
+        if (s.rcp_ok & 8) {
+            sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
+        } else {
+            RTPB_NO_SPECULATE();
+            sin_t2 = q1 / n2;
+        }
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
@@ -586,7 +592,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
         // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
         const T k = iwl.k;
-        o.ph = rf.ph - k * n1 * pw + k * (uni ? s.nnf : n1 * n1 * f + n2 * n2 * f);
+        o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
         after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
                          static_cast<const Rcp<T>*>(nullptr), g);
     } else {
@@ -611,7 +617,14 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
             kill_if(r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0), ri);
             emit_at(ri);
-            after = snell(ri, Nx, Ny, Nz, (s.rcp_ok & 4) ? s.nr : n1 / n2, g);
+            T ratio;
+            if (s.rcp_ok & 4) {
+                ratio = s.nr;
+            } else {
+                RTPB_NO_SPECULATE();
+                ratio = n1 / n2;
+            }
+            after = snell(ri, Nx, Ny, Nz, ratio, g);
             const bool ok = (KIND == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
             kill_if(!ok, after);
         }
@@ -764,8 +777,6 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     for (int j = 0; j < 3; ++j) d.nf[j] = s.normal[j] * s.focal_len;     // RT:1682-1687 `normal * focal_len`
     d.nr = 0.0;
     d.rn2 = 0.0;
-    for (int j = 0; j < 3; ++j) d.F[j] = d.B[j] = 0.0;
-    d.n1f = d.nnf = 0.0;
     return d;
 }
 
@@ -773,19 +784,9 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
 // Constant (MAT:72-79: n does not depend on the wavelength, NaN included).
 inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>& m1, const DevMaterial<double>& m2) {
     if (m1.kind == CONSTANT && m2.kind == CONSTANT) {
-        const double n1 = m1.c[0], n2 = m2.c[0], f = d.f;
-        d.nr = n1 / n2;
-        d.rn2 = 1.0 / n2;
-        d.rcp_ok |= 4 | (host_rcp_ok(n2) ? 8 : 0);
-        if (d.kind == PERFECT_LENS) {            // the per-ray expressions of surface_step, evaluated once
-            for (int j = 0; j < 3; ++j) {
-                d.F[j] = d.c[j] - d.nf[j] * n1;
-                d.B[j] = d.c[j] + d.nf[j] * n2;
-            }
-            d.n1f = n1 * f;
-            d.nnf = n1 * n1 * f + n2 * n2 * f;
-            d.rcp_ok |= 16;
-        }
+        d.nr = m1.c[0] / m2.c[0];
+        d.rn2 = 1.0 / m2.c[0];
+        d.rcp_ok |= 4 | (host_rcp_ok(m2.c[0]) ? 8 : 0);
     }
 }
 

@@ -44,6 +44,11 @@ VARIANTS = {
         "rtpb_trace_kernel.h",
         "    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);",
         "    else r = load_ray<TIN, IN_LAYOUT>(a.in, (valid ? i : a.n - 1) & ((1 << 20) - 1), a.in_fs);")]),
+    # float32 history kernels held to >= 6 waves per SIMD (<= 80 VGPRs)
+    "wpe6hist": (False, [], [(
+        "rtpb_trace_kernel.h",
+        "#define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? 6 : 1)",
+        "#define RTPB_WPE(F) ((((ST & 8) && sizeof(T) == 8) || (!(ST & 8) && sizeof(T) == 4)) && (F) != 15 ? 6 : 1)")]),
     # round-3 math changes, one at a time reverted (bit-identical variants)
     "oldchk": (False, [], [(
         "rtpb_math.h",

@@ -6,6 +6,7 @@ tests whether a history kernel is power-limited (DVFS) rather than bound by HBM 
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 import threading
@@ -41,11 +42,10 @@ def parse(txt):
                 power = float(v)
             except ValueError:
                 pass
-        if kl.startswith("sclk") or "sclk clock" in kl:
-            try:
-                clock = float(str(v).strip("()Mhz").split("Mhz")[0])
-            except ValueError:
-                pass
+        if "sclk" in kl:
+            m = re.search(r"\((\d+)\s*mhz\)", str(v).lower())
+            if m:
+                clock = float(m.group(1))
     return power, clock
 
 
