@@ -170,8 +170,9 @@ RTPB_HD void kill_if(bool c, Ray<T>& r) {
     if (c) kill(r);
 }
 
-// Selects a value by a wave-uniform descriptor bit as a real (scalar) branch: the empty volatile asm keeps
-// the compiler from speculating the per-lane computation into a select, which would run it on every path.
+// Selects a value by a wave-uniform descriptor bit as a real (scalar) branch: the empty volatile asm in the
+// (cheap) uniform side keeps the compiler from folding the diamond into a select that computes the per-lane
+// side on every path; the per-lane side keeps its normal scheduling.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define RTPB_NO_SPECULATE() asm volatile("")
 #else
@@ -578,9 +579,9 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         const T q1 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
         T sin_t2;
         if (s.rcp_ok & 8) {
+            RTPB_NO_SPECULATE();
             sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
         } else {
-            RTPB_NO_SPECULATE();
             sin_t2 = q1 / n2;
         }
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
@@ -619,9 +620,9 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             emit_at(ri);
             T ratio;
             if (s.rcp_ok & 4) {
+                RTPB_NO_SPECULATE();
                 ratio = s.nr;
             } else {
-                RTPB_NO_SPECULATE();
                 ratio = n1 / n2;
             }
             after = snell(ri, Nx, Ny, Nz, ratio, g);
