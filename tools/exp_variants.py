@@ -27,7 +27,7 @@ VARIANTS = {
     # the memory path alone: the surface arithmetic replaced by a copy (same loads, tiles and stores)
     "nocomp": (False, [], [(
         "rtpb_trace_kernel.h",
-        "        propagate_surface_emit<T, kLens>(load_surface<T>(surf + s), r, n_cur, n_next, iwl, emit_at, after);",
+        "        propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_next, iwl, emit_at, after);",
         "        after = r; after.ph = r.ph + n_next + n_cur; emit_at(r);")]),
     # the compute side alone: LDS staging kept, global history stores dropped (the tile reads are kept
     # alive), i.e. what the kernel costs without the HBM write stream
