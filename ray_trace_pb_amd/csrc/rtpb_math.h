@@ -146,7 +146,8 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     }
 }
 
-template <typename T> RTPB_HD T tabs(T v) { return v < T(0) ? -v : (v == T(0) ? T(0) : v); }
+// numpy.abs: |v| with +0 for -0 -- the sign-bit clear (one VALU, or a free operand modifier in a compare)
+template <typename T> RTPB_HD T tabs(T v) { return std::fabs(v); }
 
 template <typename T> RTPB_HD T tpow(T b, T e);
 template <> RTPB_HD double tpow<double>(double b, double e) { return pow(b, e); }
@@ -179,12 +180,13 @@ RTPB_HD void kill_if(bool c, Ray<T>& r) {
 #define RTPB_NO_SPECULATE() ((void)0)
 #endif
 
-// NaN-propagating minimum, numpy.minimum / numpy.min semantics
+// 0 <= v < inf, -0 included (v a zero, positive denormal or positive normal number)
 template <typename T>
-RTPB_HD T nan_min(T a, T b) {
-    if (is_nan(a)) return a;
-    if (is_nan(b)) return b;
-    return b < a ? b : a;
+RTPB_HD bool nonneg_finite(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, 0x1E0);    // -0 | +0 | +denormal | +normal
+#endif
+    return v >= T(0) && v < T(1) / T(0);
 }
 
 // numpy.sign: -1, 0, +1, NaN
@@ -329,6 +331,35 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
     x = x / r.b; y = y / r.b; z = z / r.b;
 }
 
+// (x, y, z) / r.b where r.b = RN(sqrt((x x + y y) + z z)), the vector's own norm.  Each |component| is at
+// most the norm (up to rounding) when the norm is finite, so with r.ok the numerators need only the lower
+// bound of the exact range (frexp exponent >= -799; 0, inf and NaN give 0): one min3 for the three instead
+// of three two-sided tests.  A norm of 0, inf or NaN is in r.ok's range and div_fixup returns the IEEE
+// quotient for those divisors whatever the numerator.
+template <typename T, class G = GuardBranch>
+RTPB_HD void div3_norm(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
+#if defined(RTPB_FASTDIV)
+    if constexpr (sizeof(T) == 8) {
+        const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
+        const int e = std::min(std::min(__builtin_amdgcn_frexp_exp(x), __builtin_amdgcn_frexp_exp(y)),
+                               __builtin_amdgcn_frexp_exp(z));
+        const bool slow = !(r.ok && e >= -799);
+        if constexpr (G::kDefer) {
+            g->bad = g->bad || slow;
+        } else {
+            if (__builtin_expect(slow, 0)) {
+                x = x / r.b; y = y / r.b; z = z / r.b;
+                return;
+            }
+        }
+        x = qx; y = qy; z = qz;
+        return;
+    }
+#endif
+    (void)g;
+    x = x / r.b; y = y / r.b; z = z / r.b;
+}
+
 // ------------------------------------------------------------------ Material.n (MAT:39-144)
 // WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
 // budget); WITH_TABLE = false compiles the TABLE case out.  Either is only valid for plans without such
@@ -426,13 +457,13 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ox * ox + oy * oy + oz * oz - s.R2;
     const T root = tsqrt<T>(B * B - T(4) * C, g);
-    T t1 = T(0.5) * (-B + root);
-    T t2 = T(0.5) * (-B - root);
-    const T inf = T(1) / T(0);
-    if (t1 < T(0)) t1 = inf;
-    if (t2 < T(0)) t2 = inf;
-    T t = nan_min(t1, t2);
-    if (t == inf) t = qnan<T>();
+    const T t1 = T(0.5) * (-B + root);
+    const T t2 = T(0.5) * (-B - root);
+    // The reference: negative roots -> inf, nan-propagating min, inf -> NaN.  root is >= +0 or NaN, so where
+    // both roots are numbers t2 <= t1; t2 is NaN only with t1 NaN or +inf.  Hence: t2 when 0 <= t2 < t1,
+    // else t1, and NaN unless the choice is in [0, inf) -- the same value, zero signs included.
+    T t = (t2 >= T(0) && t2 < t1) ? t2 : t1;
+    if (!nonneg_finite(t)) t = qnan<T>();
     Ray<T> o;
     o.x = r.x + r.dx * t;
     o.y = r.y + r.dy * t;
@@ -458,7 +489,7 @@ RTPB_HD bool positive_finite(T v) {
 template <typename T, class G = GuardBranch>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
     const T nrm = tsqrt<T>(x * x + y * y + z * z, g);
-    div3(x, y, z, make_rcp(nrm), g);
+    div3_norm(x, y, z, make_rcp(nrm), g);
     // A NaN quotient needs a zero, infinite or NaN norm: when 0 < |v| < inf every component is finite and
     // every quotient a number, so one class test skips the three per-component fix-ups (normal incidence,
     // dead rows and garbage input take them)
@@ -489,8 +520,12 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr
     T cx, cy, cz;
     tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
-    const T sgn = np_sign<T>(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
-    const T tang = sgn * tsqrt<T>(T(1) - mag * mag, g);
+    const T v = Nx * ri.dx + Ny * ri.dy + Nz * ri.dz;
+    const T root = tsqrt<T>(T(1) - mag * mag, g);
+    // np.sign(v) * root: root is >= +0 or NaN (1 - m^2 is never -0), so for v < 0 or v > 0 the product is
+    // root carrying v's sign; v = +-0 and NaN keep the product itself
+    T tang = std::copysign(root, v);
+    if (__builtin_expect(!(v < T(0) || v > T(0)), 0)) tang = np_sign<T>(v) * root;
     Ray<T> o;
     o.dx = mag * cx + tang * Nx;
     o.dy = mag * cy + tang * Ny;
@@ -565,11 +600,11 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
         T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
         const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz, g);
-        if (spn > T(1e-12)) div3(spx, spy, spz, make_rcp(spn), g);
+        if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
         const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
         const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z, g);
         T ux = r1x, uy = r1y, uz = r1z;
-        if (r1n != T(0)) div3(ux, uy, uz, make_rcp(r1n), g);
+        if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
         const T h = n1 * f * sin_t1;

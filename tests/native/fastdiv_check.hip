@@ -1,5 +1,5 @@
 // fastdiv_check.hip -- TEST INFRASTRUCTURE ONLY: runs the shared-divisor quotient helpers of
-// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3) and its square root (tsqrt) on the GPU over caller-supplied
+// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3 / div3_norm) and its square root (tsqrt) on the GPU over caller-supplied
 // operand pairs, next to the compiler's own `a / b`, so tests/test_gpu_fastdiv.py can check that every
 // quotient is bit-identical to the IEEE division (NumPy's a / b) on adversarial inputs.
 //
@@ -13,13 +13,14 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kOut = 19;
+constexpr int kOut = 26;
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
 //      [8] div1(a, host_rcp(b, yh)) with yh = the host's RN(1 / b) (the descriptors' rR / rf),
 //      then the GuardDefer forms (no fallback branch; a flag instead): [9] div1, [10] its flag,
-//      [11..13] div3, [14] its flag, [15] tsqrt(b), [16] its flag, [17] div1_as, [18] its flag
+//      [11..13] div3, [14] its flag, [15] tsqrt(b), [16] its flag, [17] div1_as, [18] its flag,
+//      [19..21] div3_norm((a, a2, a3), rcp(their norm)), [22..24] its GuardDefer form, [25] that flag
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -53,6 +54,19 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[16 * n + i] = g3.bad ? 1.0 : 0.0;
     out[17 * n + i] = div1_as(ai, bb, r, &g4);
     out[18 * n + i] = g4.bad ? 1.0 : 0.0;
+    double ux = ai, uy = a2[i], uz = a3[i];
+    const Rcp<double> rn = make_rcp(tsqrt<double>(ux * ux + uy * uy + uz * uz));
+    div3_norm(ux, uy, uz, rn);
+    out[19 * n + i] = ux;
+    out[20 * n + i] = uy;
+    out[21 * n + i] = uz;
+    GuardDefer g5;
+    double vx = ai, vy = a2[i], vz = a3[i];
+    div3_norm(vx, vy, vz, rn, &g5);
+    out[22 * n + i] = vx;
+    out[23 * n + i] = vy;
+    out[24 * n + i] = vz;
+    out[25 * n + i] = g5.bad ? 1.0 : 0.0;
 }
 
 }  // namespace

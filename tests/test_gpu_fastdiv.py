@@ -1,4 +1,4 @@
-"""The kernels' shared-divisor quotients (rtpb_math.h make_rcp / div1 / div1_as / div3) and square root
+"""The kernels' shared-divisor quotients (rtpb_math.h make_rcp / div1 / div1_as / div3 / div3_norm) and square root
 (tsqrt) are bit-identical to IEEE division and sqrt (NumPy's a / b, np.sqrt) on the GPU -- including the sign of zero -- on adversarial operands:
 random bit patterns over the whole double range, operands straddling the fast-path range limits,
 denormals, 0 / inf / NaN combinations, and realistic normalisation inputs (vector components over
@@ -33,11 +33,16 @@ def _check(a, a2, a3, b, kill):
         _same(out[6], np.sqrt(b))        # tsqrt
         _same(out[7], np.sqrt(a))
         _same(out[8], a / b)             # div1 with the host's reciprocal (descriptor rR / rf)
+        nrm = np.sqrt(a * a + a2 * a2 + a3 * a3)   # div3_norm: the vector over its own norm
+        _same(out[19], a / nrm)
+        _same(out[20], a2 / nrm)
+        _same(out[21], a3 / nrm)
         # GuardDefer: no fallback branch; where the flag is clear the value is the exact one, and the
         # flag is set only where an operand left the shortcut's exact range (the flagged rays are re-traced)
         for val, flag, exp in ((out[9], out[10], a / b), (out[11], out[14], a / b), (out[12], out[14], a2 / b),
                                (out[13], out[14], a3 / b), (out[15], out[16], np.sqrt(b)),
-                               (out[17], out[18], a / bb)):
+                               (out[17], out[18], a / bb), (out[22], out[25], a / nrm),
+                               (out[23], out[25], a2 / nrm), (out[24], out[25], a3 / nrm)):
             ok = flag == 0
             _same(val[ok], exp[ok])
         return out
@@ -101,7 +106,7 @@ def test_deferred_guards_flag_only_out_of_range_operands():
     b[::103] = np.inf
     kill = np.zeros(n, dtype=np.uint8)
     out = _check(a, a * 0.5, -a, b, kill)
-    for f in (10, 14, 16, 18):
+    for f in (10, 14, 16, 18):          # (25: div3_norm divides by the norm of (a, a / 2, -a), up to 2^300)
         assert not out[f].any(), (f, int(out[f].sum()))
 
 
