@@ -128,8 +128,9 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     double s3 = __builtin_fma(d1, h1, s2);
     // the set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
     // compare of the high word (negative values and NaN have it at or above 0x10000000 unsigned)
-    const bool slow = __builtin_amdgcn_class(v, 0x2E0) ||
-                      static_cast<uint32_t>(__double2hiint(v)) < 0x10000000u;
+    // (bitwise |: both tests are one VALU each; a short-circuit || puts the core under a branch of its own)
+    const bool special = __builtin_amdgcn_class(v, 0x2E0);
+    const bool slow = special | (static_cast<uint32_t>(__double2hiint(v)) < 0x10000000u);
     if constexpr (G::kDefer) {
         // +-0 and +inf (normal incidence gives sqrt(0) on every axial ray) are their own square roots:
         // a select, so only 0 < v < 2^-767 is left to the re-trace
@@ -267,7 +268,8 @@ RTPB_HD T div1(T a, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, r.b, r.y);
-        const bool slow = !(r.ok && fastdiv_num_ok(a));
+        const bool num_ok = fastdiv_num_ok(a);
+        const bool slow = !(r.ok & num_ok);     // bitwise: no short-circuit branch around the fast path
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
@@ -287,7 +289,8 @@ RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, b, r.y);
-        const bool slow = !(r.ok && fastdiv_num_ok(a));
+        const bool num_ok = fastdiv_num_ok(a);
+        const bool slow = !(r.ok & num_ok);     // bitwise: no short-circuit branch around the fast path
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
@@ -314,7 +317,8 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
-        const bool slow = !(r.ok && fastdiv_num_ok(x) && fastdiv_num_ok(y) && fastdiv_num_ok(z));
+        const bool ox = fastdiv_num_ok(x), oy = fastdiv_num_ok(y), oz = fastdiv_num_ok(z);
+        const bool slow = !(r.ok & ox & oy & oz);
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
@@ -343,7 +347,7 @@ RTPB_HD void div3_norm(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
         const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
         const int e = std::min(std::min(__builtin_amdgcn_frexp_exp(x), __builtin_amdgcn_frexp_exp(y)),
                                __builtin_amdgcn_frexp_exp(z));
-        const bool slow = !(r.ok && e >= -799);
+        const bool slow = !(r.ok & (e >= -799));
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
