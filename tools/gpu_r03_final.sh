@@ -22,6 +22,7 @@ step bench 900 python bench.py --steps 20 --warmup 5
 step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof -o bench -- python3 bench.py --cpu-baseline off --traffic off --steps 20 --warmup 5
 step pmc_c4 900 bash tools/pmc_kernel.sh $P/pmc_c4 trace_kernel python3 tools/run_variant.py --config c4:1.0 --reps 2
 step pmc_c3 900 bash tools/pmc_kernel.sh $P/pmc_c3 trace_kernel python3 tools/run_variant.py --config c3:1.0 --reps 2
+step pmc_c5 900 bash tools/pmc_kernel.sh $P/pmc_c5 sweep_kernel python3 tools/c5_sweep.py --fields 1 --warmup 0
 step power 600 bash tools/gpu_r03_power.sh ${1:-r03_final}/power
 step bench2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 3
 exit 0
