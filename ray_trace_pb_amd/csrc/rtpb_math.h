@@ -455,19 +455,27 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
 }
 
 // ------------------------------------------------------------------ SphericalSurface.get_intersect (RT:1479-1516)
+// The intersection parameter from B and root = sqrt(B^2 - 4C): t1 = (-B + root) / 2, t2 = (-B - root) / 2,
+// negative roots -> inf, then numpy's min over (t1, t2) -- NaN-propagating, and the SECOND operand on a tie
+// (min(+0, -0) is -0) -- and inf -> NaN (RT:1497-1505).  root is >= +0 or NaN (B^2 - 4C is never -0), so
+// where both roots are numbers t2 <= t1, and t2 is NaN only with t1 NaN or +inf.  Hence: t2 when t2 >= 0,
+// else t1, and NaN unless the choice is in [0, inf) -- the same value, zero signs included
+// (tests/test_gpu_fastdiv.py checks it against the reference's chain on adversarial B, root).
+template <typename T>
+RTPB_HD T sphere_root(T B, T root) {
+    const T t1 = T(0.5) * (-B + root);
+    const T t2 = T(0.5) * (-B - root);
+    T t = t2 >= T(0) ? t2 : t1;
+    if (!nonneg_finite(t)) t = qnan<T>();
+    return t;
+}
+
 template <typename T, class G = GuardBranch>
 RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr) {
     const T ox = r.x - s.c[0], oy = r.y - s.c[1], oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ox * ox + oy * oy + oz * oz - s.R2;
-    const T root = tsqrt<T>(B * B - T(4) * C, g);
-    const T t1 = T(0.5) * (-B + root);
-    const T t2 = T(0.5) * (-B - root);
-    // The reference: negative roots -> inf, nan-propagating min, inf -> NaN.  root is >= +0 or NaN, so where
-    // both roots are numbers t2 <= t1; t2 is NaN only with t1 NaN or +inf.  Hence: t2 when 0 <= t2 < t1,
-    // else t1, and NaN unless the choice is in [0, inf) -- the same value, zero signs included.
-    T t = (t2 >= T(0) && t2 < t1) ? t2 : t1;
-    if (!nonneg_finite(t)) t = qnan<T>();
+    const T t = sphere_root(B, tsqrt<T>(B * B - T(4) * C, g));
     Ray<T> o;
     o.x = r.x + r.dx * t;
     o.y = r.y + r.dy * t;
@@ -517,6 +525,15 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
     unit_or_zero(cx, cy, cz, g);
 }
 
+// np.sign(v) * root for root >= +0 or NaN (RT:1217; 1 - m^2 is never -0): for v < 0 or v > 0 the product is
+// root carrying v's sign (one bit operation); v = +-0 and NaN keep the product itself
+template <typename T>
+RTPB_HD T signed_root(T v, T root) {
+    T r = std::copysign(root, v);
+    if (__builtin_expect(!(v < T(0) || v > T(0)), 0)) r = np_sign<T>(v) * root;
+    return r;
+}
+
 // Snell refraction of the intersected ray (RT:1197-1221)
 // ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
 template <typename T, class G = GuardBranch>
@@ -524,12 +541,7 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr
     T cx, cy, cz;
     tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
-    const T v = Nx * ri.dx + Ny * ri.dy + Nz * ri.dz;
-    const T root = tsqrt<T>(T(1) - mag * mag, g);
-    // np.sign(v) * root: root is >= +0 or NaN (1 - m^2 is never -0), so for v < 0 or v > 0 the product is
-    // root carrying v's sign; v = +-0 and NaN keep the product itself
-    T tang = std::copysign(root, v);
-    if (__builtin_expect(!(v < T(0) || v > T(0)), 0)) tang = np_sign<T>(v) * root;
+    const T tang = signed_root(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz, tsqrt<T>(T(1) - mag * mag, g));
     Ray<T> o;
     o.dx = mag * cx + tang * Nx;
     o.dy = mag * cy + tang * Ny;

@@ -1,5 +1,6 @@
 // fastdiv_check.hip -- TEST INFRASTRUCTURE ONLY: runs the shared-divisor quotient helpers of
-// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3 / div3_norm) and its square root (tsqrt) on the GPU over caller-supplied
+// ray_trace_pb_amd/csrc/rtpb_math.h (make_rcp / div1 / div1_as / div3 / div3_norm), its square root (tsqrt) and
+// the sphere-root choice and Snell sign (sphere_root / signed_root) on the GPU over caller-supplied
 // operand pairs, next to the compiler's own `a / b`, so tests/test_gpu_fastdiv.py can check that every
 // quotient is bit-identical to the IEEE division (NumPy's a / b) on adversarial inputs.
 //
@@ -13,14 +14,15 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kOut = 26;
+constexpr int kOut = 28;
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
 //      [8] div1(a, host_rcp(b, yh)) with yh = the host's RN(1 / b) (the descriptors' rR / rf),
 //      then the GuardDefer forms (no fallback branch; a flag instead): [9] div1, [10] its flag,
 //      [11..13] div3, [14] its flag, [15] tsqrt(b), [16] its flag, [17] div1_as, [18] its flag,
-//      [19..21] div3_norm((a, a2, a3), rcp(their norm)), [22..24] its GuardDefer form, [25] that flag
+//      [19..21] div3_norm((a, a2, a3), rcp(their norm)), [22..24] its GuardDefer form, [25] that flag,
+//      [26] sphere_root(B = a, root = tsqrt(|b|)), [27] signed_root(a, tsqrt(|b|))
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -67,6 +69,9 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[23 * n + i] = vy;
     out[24 * n + i] = vz;
     out[25 * n + i] = g5.bad ? 1.0 : 0.0;
+    const double rt = tsqrt<double>(fabs(bi));          // >= +0, +inf or NaN, as sqrt(B^2 - 4C) / sqrt(1 - m^2)
+    out[26 * n + i] = sphere_root(ai, rt);
+    out[27 * n + i] = signed_root(ai, rt);
 }
 
 }  // namespace

@@ -37,6 +37,14 @@ def _check(a, a2, a3, b, kill):
         _same(out[19], a / nrm)
         _same(out[20], a2 / nrm)
         _same(out[21], a3 / nrm)
+        # the sphere's root choice and Snell's np.sign(v) * root against the reference's own chains
+        root = np.sqrt(np.abs(b))
+        t1, t2 = 0.5 * (-a + root), 0.5 * (-a - root)          # RT:1497-1505 (oracle sphere_hit)
+        t1 = np.where(t1 < 0, np.inf, t1)
+        t2 = np.where(t2 < 0, np.inf, t2)
+        t = np.minimum(t1, t2)
+        _same(out[26], np.where(t == np.inf, np.nan, t))
+        _same(out[27], np.sign(a) * root)                       # RT:1217
         # GuardDefer: no fallback branch; where the flag is clear the value is the exact one, and the
         # flag is set only where an operand left the shortcut's exact range (the flagged rays are re-traced)
         for val, flag, exp in ((out[9], out[10], a / b), (out[11], out[14], a / b), (out[12], out[14], a2 / b),

@@ -44,6 +44,16 @@ VARIANTS = {
         "rtpb_trace_kernel.h",
         "    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);",
         "    else r = load_ray<TIN, IN_LAYOUT>(a.in, (valid ? i : a.n - 1) & ((1 << 20) - 1), a.in_fs);")]),
+    # float64 input records of a float32 history read through the wave's two float32 tiles (4 KiB: one
+    # coalesced 1 KiB load per instruction, then each lane reads its record from LDS) instead of four
+    # 16-byte loads per lane at a 64-byte lane stride
+    "stagein": (False, [], [(
+        "rtpb_trace_kernel.h",
+        "    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);",
+        "    else if constexpr (kStaged && !kFinal && !kXchg && IN_LAYOUT == RTPB_AOS && sizeof(TIN) == 8 &&\n"
+        "                       sizeof(TS) == 4)\n"
+        "        r = tile_load<TIN>(tile_a, a.in, ray0, a.n, lane);\n"
+        "    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);")]),
     # float32 history kernels held to >= 6 waves per SIMD (<= 80 VGPRs)
     "wpe6hist": (False, [], [(
         "rtpb_trace_kernel.h",
