@@ -20,6 +20,24 @@ def load_case(name):
     return spec, d["rays_in"], d["history"]
 
 
+def same_bits(got, ref):
+    """Bit-identical: equal shapes, NaN exactly where ref has NaN, and every other element the same bit
+    pattern (so +0 and -0 differ; np.array_equal with equal_nan=True treats them as equal).  Float arrays
+    of different widths are compared after an exact widening to the wider type."""
+    got, ref = np.asarray(got), np.asarray(ref)
+    if got.shape != ref.shape:
+        return False
+    if not (np.issubdtype(got.dtype, np.floating) and np.issubdtype(ref.dtype, np.floating)):
+        return bool(np.array_equal(got, ref))
+    t = np.result_type(got.dtype, ref.dtype)
+    got, ref = got.astype(t, copy=False), ref.astype(t, copy=False)
+    nan = np.isnan(ref)
+    if not np.array_equal(np.isnan(got), nan):
+        return False
+    u = {2: np.uint16, 4: np.uint32, 8: np.uint64}[t.itemsize]
+    return bool(np.array_equal(np.ascontiguousarray(got[~nan]).view(u), np.ascontiguousarray(ref[~nan]).view(u)))
+
+
 def compare(got, ref, rtol):
     """NaN masks must be equal element for element; finite values must satisfy
     |got - ref| <= rtol * max(|ref|, colmax) where colmax is the max |finite ref| of that column in

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from oracle import rt_refcost as RC
-from parity import CASES, load_case
+from parity import same_bits, CASES, load_case
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -12,7 +12,7 @@ def test_refcost_port_matches_reference_bitwise(name):
     spec, rays, ref = load_case(name)
     got = RC.ray_trace(spec["surfaces"], spec["materials"], rays)
     assert got.shape == ref.shape
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 def test_refcost_port_input_ranks():
@@ -23,4 +23,4 @@ def test_refcost_port_input_ranks():
     spec = json.loads(str(d["system_json"]))
     for k in ("1", "2", "3"):
         got = RC.ray_trace(spec["surfaces"], spec["materials"], d["rays" + k])
-        assert np.array_equal(got, d["out" + k], equal_nan=True), k
+        assert same_bits(got, d["out" + k]), k

@@ -7,6 +7,7 @@ import socket
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
+from parity import same_bits  # noqa: E402
 
 
 def _free_port():
@@ -59,6 +60,6 @@ def test_two_rank_sharded_trace_equals_unsharded(tmp_path):
     low = E.lower(system.surfaces, [m0] + list(system.materials) + [m1], lambda: np.unique(rays[:, 7]), C.RTPB_F64)
     ref = harness_trace(low, rays)
     for r in range(world):
-        assert np.array_equal(np.load(tmp_path / f"full{r}.npy"), ref, equal_nan=True)
+        assert same_bits(np.load(tmp_path / f"full{r}.npy"), ref)
     parts = [np.load(tmp_path / f"local{r}.npy") for r in range(world)]
-    assert np.array_equal(np.concatenate(parts, axis=1), ref, equal_nan=True)
+    assert same_bits(np.concatenate(parts, axis=1), ref)

@@ -19,7 +19,7 @@ import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from ray_trace_pb_amd import _engine as E  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
-from parity import CASES, GOLDEN  # noqa: E402
+from parity import same_bits, CASES, GOLDEN  # noqa: E402
 from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -126,6 +126,6 @@ def test_c_abi_variant_matrix(name, knob):
                                                  len(sel), out_code, out_layout)
                             key = (out_code, in_code, in_layout, out_layout, sname)
                             assert pad_ok, key
-                            assert np.array_equal(got, expect[sel], equal_nan=True), key
+                            assert same_bits(got, expect[sel]), key
                             checked += 1
     assert checked == 2 * 3 * 2 * 3

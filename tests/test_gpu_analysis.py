@@ -11,7 +11,7 @@ import ray_trace_pb_amd.materials as mat  # noqa: E402
 import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import analysis  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
-from parity import GOLDEN  # noqa: E402
+from parity import same_bits, GOLDEN  # noqa: E402
 from serialize import material_to_dict, surface_to_dict  # noqa: E402
 import systems  # noqa: E402
 
@@ -36,10 +36,10 @@ def test_device_collimated_rays_match_host(kw):
 def test_device_intersect_rays_bitwise_vs_reference():
     g = np.load(os.path.join(GOLDEN, "generators.npz"))
     got = rt.intersect_rays(torch.from_numpy(g["intersect_in1"]).to(DEV), torch.from_numpy(g["intersect_in2"]).to(DEV))
-    assert np.array_equal(got.cpu().numpy(), g["intersect_out"], equal_nan=True)
+    assert same_bits(got.cpu().numpy(), g["intersect_out"])
     fan = rt.get_ray_fan([0., 0., 0.], 0.1, 5, 0.5)
     got = rt.intersect_rays(torch.from_numpy(fan[1]).to(DEV), torch.from_numpy(fan).to(DEV))
-    assert np.array_equal(got.cpu().numpy(), g["intersect_fan_out"], equal_nan=True)
+    assert same_bits(got.cpu().numpy(), g["intersect_fan_out"])
 
 
 def test_device_auto_focus_style_focus_finding():
@@ -48,7 +48,7 @@ def test_device_auto_focus_style_focus_finding():
     h = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
     got = rt.intersect_rays(h[-1, 51:], h[-1, 50:51])
     ref = rt.intersect_rays(h[-1, 51:].cpu().numpy(), h[-1, 50:51].cpu().numpy())
-    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+    assert same_bits(got.cpu().numpy(), ref)
 
 
 def test_spot_stats_match_numpy():
@@ -107,15 +107,15 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     un, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=5, fused=False)
     assert fu.keys() == un.keys()
     for k in fu:
-        assert np.array_equal(fu[k], un[k], equal_nan=True), k
+        assert same_bits(fu[k], un[k]), k
     assert fu["count"].min() > 0
 
 
 def test_dist_pt2plane_bitwise_vs_reference():
     g = np.load(os.path.join(GOLDEN, "generators.npz"))
     dist, near = rt.dist_pt2plane(g["intersect_in1"][:, :3], np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))
-    assert np.array_equal(dist, g["dist_out"], equal_nan=True)
-    assert np.array_equal(near, g["dist_near"], equal_nan=True)
+    assert same_bits(dist, g["dist_out"])
+    assert same_bits(near, g["dist_near"])
 
 
 @pytest.mark.parametrize("exclude", [False, True])
@@ -136,8 +136,8 @@ def test_propagate_ray2plane_device_bitwise_vs_oracle(exclude):
             nn = tuple(nv[:, k] for k in range(3)) if nv.ndim == 2 else tuple(nv)
             cc = tuple(cv[:, k] for k in range(3)) if cv.ndim == 2 else tuple(cv)
             ref, tref = O.to_plane(R, nn, cc, O.refractive_index(md, R.wl), exclude)
-            assert np.array_equal(got, ref.to_array(), equal_nan=True)
-            assert np.array_equal(ts, tref, equal_nan=True)
+            assert same_bits(got, ref.to_array())
+            assert same_bits(ts, tref)
     t_out, t_ts = rt.propagate_ray2plane(torch.from_numpy(rays).to(DEV), nrm, ctr, mat.Bk7())
     assert t_out.is_cuda and t_ts.is_cuda
 
@@ -220,7 +220,7 @@ def test_spot_sweep_over_devices_is_bitwise_equal():
         many, tm = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields, wls, theta, nt, nph,
                                        devices=devs, groups_per_batch=4)
         for k in ("count", "centroid", "rms_radius"):
-            assert np.array_equal(many[k], one[k], equal_nan=True), (devs, k)
+            assert same_bits(many[k], one[k]), (devs, k)
         assert [p["device"] for p in tm["per_device"]] == devs
         assert sum(p["rays"] for p in tm["per_device"]) == t1["rays"]
         assert all(p["kernel_ms"] > 0 for p in tm["per_device"])
@@ -297,4 +297,4 @@ def test_spot_sweep_sums_bitwise_vs_oracle(dtype):
     assert summ["count"].min() > 0
     exp = analysis.summarize(ref)
     for k in ("count", "centroid", "rms_radius"):
-        assert np.array_equal(summ[k], exp[k], equal_nan=True), k
+        assert same_bits(summ[k], exp[k]), k

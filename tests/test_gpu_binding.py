@@ -14,7 +14,7 @@ import ray_trace_pb_amd.materials as mat  # noqa: E402
 import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
-from parity import CASES, GOLDEN  # noqa: E402
+from parity import same_bits, CASES, GOLDEN  # noqa: E402
 from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
 import reference_binding  # noqa: E402
 import systems  # noqa: E402
@@ -34,7 +34,7 @@ def test_binding_reproduces_reference_histories(ray_trace_gpu, name):
     system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
     got = ray_trace_gpu(system, d["rays_in"], m0, m1)
     assert got.dtype == np.float64 and got.shape == d["history"].shape
-    assert np.array_equal(got, d["history"], equal_nan=True)
+    assert same_bits(got, d["history"])
 
 
 def test_binding_input_ranks_and_history_extension(ray_trace_gpu):
@@ -42,7 +42,7 @@ def test_binding_input_ranks_and_history_extension(ray_trace_gpu):
     system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
     for k in ("1", "2", "3"):
         got = ray_trace_gpu(system, d["rays" + k], m0, m1)
-        assert got.shape == d["out" + k].shape and np.array_equal(got, d["out" + k], equal_nan=True), k
+        assert got.shape == d["out" + k].shape and same_bits(got, d["out" + k]), k
 
 
 def test_binding_surface_and_material_subclasses(ray_trace_gpu):
@@ -65,7 +65,7 @@ def test_binding_surface_and_material_subclasses(ray_trace_gpu):
         kinds = [reference_binding._builtin_kind(rt, s) for s in surfs]
         assert (None in kinds) == (cls is HookedFlat)
         got = ray_trace_gpu(rt.System(surfs, system.materials), d["rays_in"], m0, m1)
-        assert np.array_equal(got, d["history"], equal_nan=True), cls.__name__
+        assert same_bits(got, d["history"]), cls.__name__
 
 
 def test_binding_chains_launches_beyond_63_surfaces(ray_trace_gpu):
@@ -75,4 +75,4 @@ def test_binding_chains_launches_beyond_63_surfaces(ray_trace_gpu):
     ref = O.ray_trace([surface_to_dict(s) for s in system.surfaces],
                       [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]], rays)
     got = ray_trace_gpu(system, rays, m0, m1)
-    assert got.shape == ref.shape and np.array_equal(got, ref, equal_nan=True)
+    assert got.shape == ref.shape and same_bits(got, ref)

@@ -15,6 +15,7 @@ import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from ray_trace_pb_amd import _engine as E  # noqa: E402
 import systems  # noqa: E402
+from parity import same_bits  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -62,9 +63,9 @@ def test_shutdown_then_trace_again():
     E.clear_plan_cache()                                      # plans must be destroyed first
     C.check(C.lib().rtpb_shutdown())
     after = system.ray_trace(rays, m0, m1)
-    assert np.array_equal(after, before, equal_nan=True)
+    assert same_bits(after, before)
     x = torch.from_numpy(rays).to(DEV)
-    assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), before, equal_nan=True)
+    assert same_bits(system.ray_trace(x, m0, m1).cpu().numpy(), before)
 
 
 GEN_CASES = {   # tests/golden/make_golden.py: the reference's own generators (RT:45-161) on these arguments

@@ -9,6 +9,7 @@ torch = pytest.importorskip("torch")
 
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from ray_trace_pb_amd import _engine as E  # noqa: E402
+from parity import same_bits  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -34,11 +35,11 @@ def test_one_colour_and_mixed_bundles(dtype):
     x = torch.from_numpy(rays).to(DEV, dtype)
     got = E._distinct_device(x[:, 7])
     exp = _ref(x[:, 7].cpu().numpy())
-    assert got.shape == exp.shape and np.array_equal(got, exp, equal_nan=True)
+    assert got.shape == exp.shape and same_bits(got, exp)
     assert np.isnan(got[-1]) and np.isnan(got).sum() == 1
     # contiguous column, and the public entry point
     col = x[:, 7].contiguous()
-    assert np.array_equal(E.distinct_wavelengths(col), exp, equal_nan=True)
+    assert same_bits(E.distinct_wavelengths(col), exp)
 
 
 def test_many_keys_fall_back_to_sort():

@@ -20,6 +20,7 @@ import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
 from serialize import material_to_dict, surface_to_dict  # noqa: E402
 import systems  # noqa: E402
+from parity import same_bits  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -34,7 +35,7 @@ def _oracle_sample(system, m0, m1, rays_dev, hist, n_check, seed):
                       rays_dev.index_select(0, it).cpu().numpy())
     got = hist.index_select(1, it).cpu().numpy()
     assert got.dtype == np.float32 and got.shape == ref.shape
-    assert np.array_equal(got, ref.astype(np.float32), equal_nan=True)
+    assert same_bits(got, ref.astype(np.float32))
 
 
 def _properties(hist, rays_dev):

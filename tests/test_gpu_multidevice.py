@@ -14,6 +14,7 @@ from ray_trace_pb_amd import _capi as C  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
 from serialize import material_to_dict, surface_to_dict  # noqa: E402
 import systems  # noqa: E402
+from parity import same_bits  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -38,17 +39,17 @@ def test_torch_bundle_scattered_over_devices_is_bitwise_equal(devs):
     system, rays, m0, m1 = systems.stress(rt, mat)
     x = torch.from_numpy(rays).to(DEV)
     ref = system.ray_trace(x, m0, m1).cpu().numpy()
-    assert np.array_equal(ref, oracle(system, m0, m1, rays), equal_nan=True)
+    assert same_bits(ref, oracle(system, m0, m1, rays))
     got = system.ray_trace(x, m0, m1, devices=devs)
-    assert got.device == x.device and np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+    assert got.device == x.device and same_bits(got.cpu().numpy(), ref)
     parts = system.ray_trace(x, m0, m1, devices=devs, gather=False)
     assert isinstance(parts, list) and len(parts) == len(devs)
     for p, d, (a, b) in zip(parts, devs, rt.shard_bounds(x.shape[0], len(devs))):
         assert p.device.index == d and p.shape[1] == b - a
-    assert np.array_equal(np.concatenate([p.cpu().numpy() for p in parts], axis=1), ref, equal_nan=True)
+    assert same_bits(np.concatenate([p.cpu().numpy() for p in parts], axis=1), ref)
     # float32 storage, final plane, SoA
     f32 = system.ray_trace(x, m0, m1, devices=devs, dtype="float32", planes="final", layout="soa")
-    assert np.array_equal(f32.cpu().numpy(), ref[-1:].astype(np.float32).transpose(0, 2, 1), equal_nan=True)
+    assert same_bits(f32.cpu().numpy(), ref[-1:].astype(np.float32).transpose(0, 2, 1))
 
 
 @pytest.mark.parametrize("devs", device_lists())
@@ -65,8 +66,7 @@ def test_per_device_fan_shards_traced_in_place(devs):
     hist = system.ray_trace(shards, m0, m1, dtype="float32")
     assert isinstance(hist, list) and all(h.device == s.device for h, s in zip(hist, shards))
     ref = oracle(system, m0, m1, host)
-    assert np.array_equal(np.concatenate([h.cpu().numpy() for h in hist], axis=1), ref.astype(np.float32),
-                          equal_nan=True)
+    assert same_bits(np.concatenate([h.cpu().numpy() for h in hist], axis=1), ref.astype(np.float32))
 
 
 @pytest.mark.parametrize("storage", ["float64", "float32"])
@@ -84,15 +84,15 @@ def test_long_system_bitwise_vs_oracle(storage):
     assert 0 < live < rays.shape[0]
     exp = ref if storage == "float64" else ref.astype(np.float32)
     got = system.ray_trace(rays, m0, m1, dtype=storage)
-    assert got.shape == (2 * S + 1, rays.shape[0], 8) and np.array_equal(got, exp, equal_nan=True)
+    assert got.shape == (2 * S + 1, rays.shape[0], 8) and same_bits(got, exp)
     x = torch.from_numpy(rays).to(DEV)
-    assert np.array_equal(system.ray_trace(x, m0, m1, dtype=storage).cpu().numpy(), exp, equal_nan=True)
+    assert same_bits(system.ray_trace(x, m0, m1, dtype=storage).cpu().numpy(), exp)
     sel = [0, 1, 125, 126, 127, 128, 200, 2 * S]
-    assert np.array_equal(system.ray_trace(rays, m0, m1, dtype=storage, planes=sel), exp[sel], equal_nan=True)
+    assert same_bits(system.ray_trace(rays, m0, m1, dtype=storage, planes=sel), exp[sel])
     fin = system.ray_trace(x, m0, m1, dtype=storage, planes="final", layout="soa")
-    assert np.array_equal(fin.cpu().numpy(), exp[-1:].transpose(0, 2, 1), equal_nan=True)
+    assert same_bits(fin.cpu().numpy(), exp[-1:].transpose(0, 2, 1))
     h3 = np.stack((rays, rays))
     got3 = system.ray_trace(h3, m0, m1)
-    assert np.array_equal(got3[2:], ref[1:], equal_nan=True)
+    assert same_bits(got3[2:], ref[1:])
     sharded = system.ray_trace(x, m0, m1, dtype=storage, devices=[0, 0])
-    assert np.array_equal(sharded.cpu().numpy(), exp, equal_nan=True)
+    assert same_bits(sharded.cpu().numpy(), exp)

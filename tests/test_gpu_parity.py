@@ -15,7 +15,7 @@ import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from ray_trace_pb_amd import _engine as E  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
-from parity import CASES, F32IN_CASES, GOLDEN, compare, load_case  # noqa: E402
+from parity import same_bits, CASES, F32IN_CASES, GOLDEN, compare, load_case  # noqa: E402
 from serialize import material_to_dict, surface_to_dict, system_from_json  # noqa: E402
 import systems  # noqa: E402
 
@@ -40,7 +40,7 @@ def test_numpy_path_bitwise_vs_reference(name):
     got = system.ray_trace(rays, m0, m1)
     assert isinstance(got, np.ndarray) and got.dtype == np.float64 and got.flags.c_contiguous
     assert got.shape == ref.shape
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -49,7 +49,7 @@ def test_device_path_bitwise_vs_reference(name):
     got = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
     torch.cuda.synchronize()
     assert got.is_cuda and got.dtype == torch.float64
-    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+    assert same_bits(got.cpu().numpy(), ref)
 
 
 def test_input_ranks_and_extend_history():
@@ -58,9 +58,9 @@ def test_input_ranks_and_extend_history():
     for k in ("1", "2", "3"):
         got = system.ray_trace(d["rays" + k], m0, m1)
         assert got.shape == d["out" + k].shape, k
-        assert np.array_equal(got, d["out" + k], equal_nan=True), k
+        assert same_bits(got, d["out" + k]), k
         got_t = system.ray_trace(torch.from_numpy(np.ascontiguousarray(d["rays" + k])).to(DEV), m0, m1)
-        assert np.array_equal(got_t.cpu().numpy(), d["out" + k], equal_nan=True), k
+        assert same_bits(got_t.cpu().numpy(), d["out" + k]), k
 
 
 def test_surface_propagate_appends_two_planes():
@@ -69,7 +69,7 @@ def test_surface_propagate_appends_two_planes():
     h = rays
     for i, s in enumerate(system.surfaces):
         h = s.propagate(h, mats[i], mats[i + 1])
-    assert np.array_equal(h, ref, equal_nan=True)
+    assert same_bits(h, ref)
 
 
 def test_large_bundle_bitwise_vs_oracle_subsample():
@@ -79,7 +79,7 @@ def test_large_bundle_bitwise_vs_oracle_subsample():
     got = system.ray_trace(rays, mat.Vacuum(), mat.Vacuum())
     idx = np.random.default_rng(0).choice(rays.shape[0], 100_000, replace=False)
     ref = oracle(system, mat.Vacuum(), mat.Vacuum(), rays[idx])
-    assert np.array_equal(got[:, idx], ref, equal_nan=True)
+    assert same_bits(got[:, idx], ref)
 
 
 def test_full_size_properties_c2():
@@ -102,19 +102,19 @@ def test_planes_final_and_subset_match_full():
     system, m0, m1, rays, ref = build_case("c5_odt")
     fin = system.ray_trace(rays, m0, m1, planes="final")
     assert fin.shape == (1,) + ref.shape[1:]
-    assert np.array_equal(fin[0], ref[-1], equal_nan=True)
+    assert same_bits(fin[0], ref[-1])
     sel = [0, 3, 4, 17, 28]
     sub = system.ray_trace(rays, m0, m1, planes=sel)
-    assert np.array_equal(sub, ref[sel], equal_nan=True)
+    assert same_bits(sub, ref[sel])
     t = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, planes=[1, 28])
-    assert np.array_equal(t.cpu().numpy(), ref[[1, 28]], equal_nan=True)
+    assert same_bits(t.cpu().numpy(), ref[[1, 28]])
 
 
 def test_soa_layout_matches_aos():
     system, m0, m1, rays, ref = build_case("stress")
     soa = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, layout="soa")
     assert tuple(soa.shape) == (ref.shape[0], 8, ref.shape[1])
-    assert np.array_equal(soa.transpose(1, 2).cpu().numpy(), ref, equal_nan=True)
+    assert same_bits(soa.transpose(1, 2).cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("knob", [("aos_staging", 0), ("nt_stores", 0), ("stage_input", 1)])
@@ -130,7 +130,7 @@ def test_tuning_variants_bitwise(knob):
         for dt, r, exp in (("float64", rays, ref), ("float32", r32, ref32.astype(np.float32)),
                            ("float32", rays, ref.astype(np.float32)), ("float64", r32, ref32)):
             got = system.ray_trace(torch.from_numpy(r).to(DEV), m0, m1, dtype=dt).cpu().numpy()
-            assert np.array_equal(got, exp, equal_nan=True), (knob, dt, r.dtype)
+            assert same_bits(got, exp), (knob, dt, r.dtype)
     finally:
         C.check(lib.rtpb_set_tuning(knob[0].encode(), default))
 
@@ -139,9 +139,9 @@ def test_sharded_host_trace_is_bitwise_equal():
     """Ray sharding over devices (here: two shards on GPU 0) gives exactly the unsharded history."""
     system, m0, m1, rays, ref = build_case("stress")
     got = system.ray_trace(rays, m0, m1, devices=[0, 0])
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
     got3 = system.ray_trace(rays, m0, m1, devices=[0, 0, 0])
-    assert np.array_equal(got3, ref, equal_nan=True)
+    assert same_bits(got3, ref)
 
 
 @pytest.mark.parametrize("name", [c for c in CASES if c.startswith("fuzz_")])
@@ -150,11 +150,11 @@ def test_fuzz_sharded_host_trace_and_float32_storage(name):
     chunked pipeline), float64 and float32 storage, all and final planes: the reference's history
     (rounded once for float32) bit for bit."""
     system, m0, m1, rays, ref = build_case(name)
-    assert np.array_equal(system.ray_trace(rays, m0, m1, devices=[0, 0, 0]), ref, equal_nan=True)
+    assert same_bits(system.ray_trace(rays, m0, m1, devices=[0, 0, 0]), ref)
     got32 = system.ray_trace(rays, m0, m1, dtype="float32", devices=[0, 0, 0])
-    assert np.array_equal(got32, ref.astype(np.float32), equal_nan=True)
+    assert same_bits(got32, ref.astype(np.float32))
     fin = system.ray_trace(rays, m0, m1, planes="final", devices=[0, 0])
-    assert np.array_equal(fin, ref[-1:], equal_nan=True)
+    assert same_bits(fin, ref[-1:])
 
 
 def test_user_material_subclass_lowers_to_table():
@@ -163,7 +163,7 @@ def test_user_material_subclass_lowers_to_table():
     system, m0, m1, rays, ref = build_case("stress")
     assert any(type(m).__name__ == "Cauchy" for m in system.materials)
     got = system.ray_trace(rays, m0, m1)
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -175,16 +175,16 @@ def test_float32_storage_of_float64_input_is_the_rounded_reference(name):
     system, m0, m1, rays, ref = build_case(name)
     exp = ref.astype(np.float32)
     got = system.ray_trace(rays, m0, m1, dtype="float32")
-    assert got.dtype == np.float32 and np.array_equal(got, exp, equal_nan=True)
+    assert got.dtype == np.float32 and same_bits(got, exp)
     ok, rep = compare(got, ref, rtol=1e-5)
     assert ok and rep["mask_flips"] == 0, rep
     x = torch.from_numpy(rays).to(DEV)
     got_t = system.ray_trace(x, m0, m1, dtype="float32")
-    assert got_t.dtype == torch.float32 and np.array_equal(got_t.cpu().numpy(), exp, equal_nan=True)
+    assert got_t.dtype == torch.float32 and same_bits(got_t.cpu().numpy(), exp)
     fin = system.ray_trace(x, m0, m1, dtype="float32", planes="final")
-    assert np.array_equal(fin.cpu().numpy(), exp[-1:], equal_nan=True)
+    assert same_bits(fin.cpu().numpy(), exp[-1:])
     soa = system.ray_trace(x, m0, m1, dtype="float32", layout="soa")
-    assert np.array_equal(soa.transpose(1, 2).cpu().numpy(), exp, equal_nan=True)
+    assert same_bits(soa.transpose(1, 2).cpu().numpy(), exp)
 
 
 @pytest.mark.parametrize("name", CASES + F32IN_CASES)
@@ -198,13 +198,13 @@ def test_float32_input_bitwise_vs_oracle_on_widened_input(name):
     exp = full.astype(np.float32)
     got = system.ray_trace(r32, m0, m1, dtype="float32")
     assert got.dtype == np.float32
-    assert np.array_equal(got, exp, equal_nan=True)
+    assert same_bits(got, exp)
     got_t = system.ray_trace(torch.from_numpy(r32).to(DEV), m0, m1, dtype="float32")
-    assert got_t.dtype == torch.float32 and np.array_equal(got_t.cpu().numpy(), exp, equal_nan=True)
+    assert got_t.dtype == torch.float32 and same_bits(got_t.cpu().numpy(), exp)
     got64 = system.ray_trace(r32, m0, m1)
-    assert got64.dtype == np.float64 and np.array_equal(got64, full, equal_nan=True)
+    assert got64.dtype == np.float64 and same_bits(got64, full)
     got64_t = system.ray_trace(torch.from_numpy(r32).to(DEV), m0, m1)
-    assert got64_t.dtype == torch.float64 and np.array_equal(got64_t.cpu().numpy(), full, equal_nan=True)
+    assert got64_t.dtype == torch.float64 and same_bits(got64_t.cpu().numpy(), full)
 
 
 @pytest.mark.parametrize("name", F32IN_CASES)
@@ -235,12 +235,12 @@ def test_float32_storage_c4_fan_40k_rays():
     killed = np.isnan(ref[-1]).all(axis=1).sum()
     assert 0 < killed < fan.shape[0]                      # the NA clip is exercised
     got = system.ray_trace(fan, m0, m1, dtype="float32")
-    assert np.array_equal(got, ref.astype(np.float32), equal_nan=True)
+    assert same_bits(got, ref.astype(np.float32))
     ok, rep = compare(got, ref, rtol=1e-5)
     assert ok and rep["mask_flips"] == 0, rep
     fan_d = rt.get_ray_fan(*args, nphis=200, device=DEV)
     got_d = system.ray_trace(fan_d, m0, m1, dtype="float32")
-    assert np.array_equal(got_d.cpu().numpy(), ref.astype(np.float32), equal_nan=True)
+    assert same_bits(got_d.cpu().numpy(), ref.astype(np.float32))
 
 
 def test_kat_perfect_lens_equal_phase():
@@ -332,7 +332,7 @@ def test_user_surface_with_own_propagate_runs_between_gpu_segments():
     custom = rt.System(surfs, system.materials)
     got = custom.ray_trace(rays, m0, m1)
     assert OracleFlat.calls == 1
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
     with pytest.raises(ValueError):
         custom.ray_trace(rays, m0, m1, planes="final")
 
@@ -457,13 +457,13 @@ def test_user_geometry_hooks_bitwise_vs_reference(name):
     assert n_user >= 1
     got = hooked.ray_trace(rays, m0, m1)
     assert got.shape == ref.shape
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
     # one surface through Surface.propagate on its own
     s0 = hooked.surfaces[0]
     if s0._rtpb_user_geometry():
         mats = [m0] + list(system.materials) + [m1]
         one = s0.propagate(rays, mats[0], mats[1])
-        assert np.array_equal(one, ref[:3], equal_nan=True)
+        assert same_bits(one, ref[:3])
 
 
 def test_user_geometry_hooks_on_device_history():
@@ -473,7 +473,7 @@ def test_user_geometry_hooks_on_device_history():
     assert any(s._rtpb_user_geometry() for s in hooked.surfaces)
     got = hooked.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
     assert got.is_cuda
-    assert np.array_equal(got.cpu().numpy(), ref, equal_nan=True)
+    assert same_bits(got.cpu().numpy(), ref)
 
 
 @pytest.mark.parametrize("material", ["Ebaf11", "Nsf11", "Bk7", "Cauchy"])
@@ -493,7 +493,7 @@ def test_material_dispersion_bitwise_over_wavelength_sweep(material):
     rays[:, 7] = rng.uniform(0.35, 2.0, n)
     got = system.ray_trace(rays, mat.Vacuum(), mat.Vacuum())
     ref = oracle(system, mat.Vacuum(), mat.Vacuum(), rays)
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 @pytest.mark.parametrize("n_wl", [1, 127, 128, 129, 255, 256, 257])
@@ -517,21 +517,21 @@ def test_table_materials_lds_and_global_lookup(n_wl):
     rays[:, 7] = wls[rng.integers(0, n_wl, n)]
     m0, m1 = mat.Vacuum(), mat.Vacuum()
     ref = oracle(system, m0, m1, rays)
-    assert np.array_equal(system.ray_trace(rays, m0, m1), ref, equal_nan=True)
+    assert same_bits(system.ray_trace(rays, m0, m1), ref)
     x = torch.from_numpy(rays).to(DEV)
-    assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), ref, equal_nan=True)
+    assert same_bits(system.ray_trace(x, m0, m1).cpu().numpy(), ref)
     r32 = rays.astype(np.float32)
     exp32 = oracle(system, m0, m1, r32.astype(np.float64)).astype(np.float32)
     got32 = system.ray_trace(torch.from_numpy(r32).to(DEV), m0, m1, dtype="float32").cpu().numpy()
-    assert np.array_equal(got32, exp32, equal_nan=True)
+    assert same_bits(got32, exp32)
     # float64 rays into float32 storage: the table keys are the rays' own float64 wavelengths
     got32_64 = system.ray_trace(x, m0, m1, dtype="float32").cpu().numpy()
-    assert np.array_equal(got32_64, ref.astype(np.float32), equal_nan=True)
+    assert same_bits(got32_64, ref.astype(np.float32))
     assert np.isfinite(got32_64[-1, :, 0]).sum() > n // 2
     lib = C.lib()
     C.check(lib.rtpb_set_tuning(b"aos_staging", 0))
     try:
-        assert np.array_equal(system.ray_trace(x, m0, m1).cpu().numpy(), ref, equal_nan=True)
+        assert same_bits(system.ray_trace(x, m0, m1).cpu().numpy(), ref)
     finally:
         C.check(lib.rtpb_set_tuning(b"aos_staging", 1))
 
@@ -555,7 +555,7 @@ def test_more_than_2_31_rays_in_one_launch():
     del rays, out
     torch.cuda.empty_cache()
     ref = oracle(system, m0, m1, r_in)[-1].astype(np.float32)
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
     assert np.isfinite(got[:, 0]).sum() > 1000        # not an all-NaN comparison
 
 
@@ -587,7 +587,7 @@ def test_concurrent_host_threads_give_identical_results():
     assert not errors, errors
     for k in range(len(cases)):
         for it in range(3):
-            assert np.array_equal(got[k][it], want[k], equal_nan=True), (cases[k], it)
+            assert same_bits(got[k][it], want[k]), (cases[k], it)
 
 
 def test_snell_and_reflection_invariants_at_full_size():

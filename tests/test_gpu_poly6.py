@@ -13,7 +13,7 @@ import ray_trace_pb_amd.materials as mat  # noqa: E402
 import ray_trace_pb_amd.raytrace as rt  # noqa: E402
 from ray_trace_pb_amd import _capi as C  # noqa: E402
 from ray_trace_pb_amd import analysis  # noqa: E402
-from parity import compare  # noqa: E402
+from parity import same_bits, compare  # noqa: E402
 import systems  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -45,7 +45,7 @@ def test_poly6_trace_matches_table_trace():
     ok, rep = compare(got, ref, rtol=1e-12)
     assert ok and rep["mask_flips"] == 0, rep
     fin = poly.ray_trace(x, m0, m1, planes="final").cpu().numpy()
-    assert np.array_equal(fin[0], got[-1], equal_nan=True)
+    assert same_bits(fin[0], got[-1])
     f32 = poly.ray_trace(x, m0, m1, dtype="float32").cpu().numpy()
     ok, rep = compare(f32, ref, rtol=1e-6)
     assert ok and rep["mask_flips"] == 0, rep

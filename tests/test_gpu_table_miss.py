@@ -16,6 +16,7 @@ from ray_trace_pb_amd import _engine as E  # noqa: E402
 from oracle import rt_numpy as O  # noqa: E402
 from serialize import material_to_dict, surface_to_dict  # noqa: E402
 import systems  # noqa: E402
+from parity import same_bits  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -63,7 +64,7 @@ def test_miss_flag_every_table_variant(variant):
         flag = torch.zeros(1, dtype=torch.int32, device=DEV)
         out = E.trace_device(low, x, sel, miss=flag)
         assert int(flag.item()) == 0
-        assert np.array_equal(out.cpu().numpy(), _oracle(system, m0, m1, rays), equal_nan=True)
+        assert same_bits(out.cpu().numpy(), _oracle(system, m0, m1, rays))
         for bad in (0.5123, np.nan):
             r2 = rays.copy()
             r2[1777, 7] = bad
@@ -78,7 +79,7 @@ def test_miss_flag_every_table_variant(variant):
         flag.zero_()
         out3 = E.trace_device(low_nan, torch.from_numpy(r3).to(DEV), sel, miss=flag)
         assert int(flag.item()) == 0
-        assert np.array_equal(out3.cpu().numpy(), _oracle(system, m0, m1, r3), equal_nan=True)
+        assert same_bits(out3.cpu().numpy(), _oracle(system, m0, m1, r3))
         # no flag pointer: the plain launch
         E.trace_device(low, x, sel)
     finally:
@@ -100,7 +101,7 @@ def test_optimistic_keys_reused_and_rescanned_on_a_miss(monkeypatch):
     def check(rays, dtype=None):
         got = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, dtype=dtype).cpu().numpy()
         ref = _oracle(system, m0, m1, rays)
-        assert np.array_equal(got, ref if dtype is None else ref.astype(np.float32), equal_nan=True)
+        assert same_bits(got, ref if dtype is None else ref.astype(np.float32))
 
     check(_rays(2049, [0.5, 0.6, 0.7], 1))
     assert len(scans) == 1
@@ -119,7 +120,7 @@ def test_optimistic_keys_reused_and_rescanned_on_a_miss(monkeypatch):
     hist = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)
     ext = system.ray_trace(hist, m0, m1).cpu().numpy()
     ref = _oracle(system, m0, m1, rays)
-    assert np.array_equal(ext[:ref.shape[0]], ref, equal_nan=True) and ext.shape[0] == 2 * ref.shape[0] - 1
+    assert same_bits(ext[:ref.shape[0]], ref) and ext.shape[0] == 2 * ref.shape[0] - 1
     fin = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1, planes="final").cpu().numpy()
-    assert np.array_equal(fin[0], ref[-1], equal_nan=True)
+    assert same_bits(fin[0], ref[-1])
     assert len(scans) == 3

@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from ray_trace_pb_amd.io import ARRAY_COLUMNS, HistoryWriter, read_array, read_attrs
+from parity import same_bits  # noqa: E402
 
 
 def test_round_trip_numpy(tmp_path):
@@ -20,7 +21,7 @@ def test_round_trip_numpy(tmp_path):
     got = read_array(p)
     assert got.shape == (5, 7, 13, 8)
     for i in range(4):
-        assert np.array_equal(got[i], hist[i], equal_nan=True)
+        assert same_bits(got[i], hist[i])
     assert np.isnan(got[4]).all()                                    # unwritten config -> fill value
     assert read_attrs(p, "rays")["array_columns"] == ARRAY_COLUMNS
     assert read_attrs(p)["settings"]["nrays"] == 13
@@ -56,7 +57,7 @@ def test_round_trip_device_histories(tmp_path):
             w.write(i, h)
     got = read_array(p)
     for i in range(3):
-        assert np.array_equal(got[i], ref[i], equal_nan=True)
+        assert same_bits(got[i], ref[i])
 
 
 LIGHTSHEET_RADII = (8.0, 120.0, 1e9)
@@ -83,7 +84,7 @@ def _check_lightsheet_store(p, histories):
     assert np.array_equal(read_array(p, "focal_lens_mm"), rc / (LIGHTSHEET_SETTINGS["n_etl"] - 1))
     got = read_array(p)
     for i, h in enumerate(histories):
-        assert np.array_equal(got[i], h, equal_nan=True), i
+        assert same_bits(got[i], h), i
 
 
 def _write_lightsheet_store(p, histories):

@@ -11,7 +11,7 @@ import ray_trace_pb_amd.raytrace as rt
 from ray_trace_pb_amd import _capi as C
 from ray_trace_pb_amd import _engine as E
 from native_harness import harness, harness_trace
-from parity import CASES, load_case
+from parity import same_bits, CASES, load_case
 from serialize import system_from_json
 import json
 
@@ -29,7 +29,7 @@ def lowered_case(name):
 def test_kernel_math_bitwise_vs_reference(name):
     low, rays, ref = lowered_case(name)
     got = harness_trace(low, rays)
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 def _up(x):

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 from oracle import rt_numpy as O
-from parity import CASES, F32IN_CASES, compare, load_case
+from parity import same_bits, CASES, F32IN_CASES, compare, load_case
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -11,7 +11,7 @@ def test_oracle_matches_reference_bitwise(name):
     spec, rays, ref = load_case(name)
     got = O.ray_trace(spec["surfaces"], spec["materials"], rays)
     assert got.shape == ref.shape
-    assert np.array_equal(got, ref, equal_nan=True)
+    assert same_bits(got, ref)
 
 
 @pytest.mark.parametrize("name", F32IN_CASES)
@@ -35,7 +35,7 @@ def test_oracle_input_ranks():
     spec = json.loads(str(d["system_json"]))
     for k in ("1", "2", "3"):
         got = O.ray_trace(spec["surfaces"], spec["materials"], d["rays" + k])
-        assert np.array_equal(got, d["out" + k], equal_nan=True), k
+        assert same_bits(got, d["out" + k]), k
 
 
 def test_oracle_generators():
