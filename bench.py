@@ -422,6 +422,24 @@ def _gather(world, vals):
     return [o.tolist() for o in out]
 
 
+def host_e2e(w, reps=3):
+    """the end-to-end rate with the PCIe transfers -- System.ray_trace on a NumPy bundle in host
+    memory returning the NumPy history (rtpb_trace_host: pinned staging, chunked H2D / trace / D2H)."""
+    host = w.rays.cpu().numpy()
+    h = w.system.ray_trace(host, w.m0, w.m1)
+    ts = []
+    for _ in range(reps):
+        del h
+        t0 = time.perf_counter()
+        h = w.system.ray_trace(host, w.m0, w.m1)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    nbytes = host.nbytes + h.nbytes
+    return {"ms": t * 1e3, "ray_surface_per_s": w.n * w.S / t, "host_bytes": nbytes, "host_GBps": nbytes / t / 1e9,
+            "note": "NumPy rays in host memory -> NumPy history (H2D + trace + D2H through rtpb_trace_host); "
+                    "never the headline value"}
+
+
 def run_c2(args, dev, copy):
     import torch
     w2 = Workload("c2", dev, 0, c2_rays=args.rays)
@@ -436,6 +454,7 @@ def run_c2(args, dev, copy):
     res = {"baseline_config": "configs[1]", "workload": w2.workload, "dtype": "f64", "storage": w2.storage,
            "value": w2.n * w2.S * steps / e2, "unit": UNIT, "n_gpus": 1, "steps": steps, "ms_per_step": e2 / steps * 1e3,
            "rays": w2.n, "surfaces": w2.S, "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate(), copy)}
+    res["host_e2e"] = host_e2e(w2)
     del w2
     torch.cuda.empty_cache()
     return res
