@@ -54,6 +54,15 @@ VARIANTS = {
         "                       sizeof(TS) == 4)\n"
         "        r = tile_load<TIN>(tile_a, a.in, ray0, a.n, lane);\n"
         "    else r = load_ray<TIN, IN_LAYOUT>(a.in, valid ? i : a.n - 1, a.in_fs);")]),
+    # history kernels allowed more registers: at most 5 / 4 waves per SIMD (the scheduler's occupancy target)
+    "wpemax5": (False, [], [(
+        "rtpb_trace_kernel.h",
+        "__attribute__((amdgpu_waves_per_eu(WPE, 8)))",
+        "__attribute__((amdgpu_waves_per_eu(WPE, (STORE & 8) ? 8 : 5)))")]),
+    "wpemax4": (False, [], [(
+        "rtpb_trace_kernel.h",
+        "__attribute__((amdgpu_waves_per_eu(WPE, 8)))",
+        "__attribute__((amdgpu_waves_per_eu(WPE, (STORE & 8) ? 8 : 4)))")]),
     # float32 history kernels held to >= 6 waves per SIMD (<= 80 VGPRs)
     "wpe6hist": (False, [], [(
         "rtpb_trace_kernel.h",
