@@ -37,7 +37,8 @@ template <typename T>
 struct DevSurface {
     int32_t kind;
     int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok); bit 2: nr
-                      // valid; bit 3: rn2 valid and usable by the quotients
+                      // valid; bit 3: rn2 valid and usable by the quotients; bits 4 / 5: bits 2 / 3 for a
+                      // boundary with a Vacuum side, valid where the wavelength squared is finite and nonzero
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -60,9 +61,10 @@ struct DevSurface {
     // PerfectLens: normal * focal_len, the host-side product of F = C - n f n1 and B = C + n f n2 (RT:1682-1687
     // evaluate `normal * self.focal_len` before the per-ray index)
     T nf[3];
-    // both adjacent media Constant (rcp_ok bit 2): n1 and n2 are the same for every ray, so the Snell ratio
-    // n1 / n2 (RT:1213) and 1 / n2 (PerfectLens sin_t2, RT:1749) are computed once on the host (IEEE
-    // division: the same correctly rounded values the per-lane divisions give)
+    // both adjacent media Constant or Vacuum (rcp_ok bit 2, or bit 4 with a Vacuum side): n1 and n2 are the
+    // same for every ray (Vacuum: 1, MAT:54-56), so the Snell ratio n1 / n2 (RT:1213) and 1 / n2
+    // (PerfectLens sin_t2, RT:1749) are computed once on the host (IEEE division: the same correctly
+    // rounded values the per-lane divisions give)
     T nr;
     T rn2;
 };
@@ -835,10 +837,20 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
 // The media on either side (the plan's device materials m1 = before, m2 = after): uniform when both are
 // Constant (MAT:72-79: n does not depend on the wavelength, NaN included).
 inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>& m1, const DevMaterial<double>& m2) {
-    if (m1.kind == CONSTANT && m2.kind == CONSTANT) {
-        d.nr = m1.c[0] / m2.c[0];
-        d.rn2 = 1.0 / m2.c[0];
-        d.rcp_ok |= 4 | (host_rcp_ok(m2.c[0]) ? 8 : 0);
+    // Constant: c0 for every ray; Vacuum: 1 for every ray whose wavelength squared is finite and nonzero
+    auto uniform_n = [](const DevMaterial<double>& m, double& n) {
+        if (m.kind == CONSTANT) { n = m.c[0]; return true; }
+        if (m.kind == VACUUM) { n = 1.0; return true; }
+        return false;
+    };
+    double n1, n2;
+    if (uniform_n(m1, n1) && uniform_n(m2, n2)) {
+        d.nr = n1 / n2;
+        d.rn2 = 1.0 / n2;
+        const int bits = 4 | (host_rcp_ok(n2) ? 8 : 0);
+        // next to a Vacuum the values hold only for ordinary wavelengths: bits 4 / 8 moved to 16 / 32, which
+        // the trace kernel turns into 4 / 8 when every ray of the wave has one
+        d.rcp_ok |= (m1.kind == VACUUM || m2.kind == VACUUM) ? bits << 2 : bits;
     }
 }
 

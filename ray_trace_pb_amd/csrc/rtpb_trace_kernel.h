@@ -122,8 +122,13 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     }
     // every lane of the wave has its key: the surfaces' Snell ratios come from the table too (uniform test)
     const bool all_idx = kIdx && __builtin_amdgcn_ballot_w64(widx < 0) == 0;
+    // every lane's Vacuum index is exactly 1 (wavelength squared finite and nonzero, MAT:54-56): the host's
+    // ratios of Constant / Vacuum boundaries hold for the whole wave (uniform test)
+    const T w2 = wl0 * wl0;
+    const bool vac_one = __builtin_amdgcn_ballot_w64(!(w2 != T(0) && w2 - w2 == T(0))) == 0;
     auto surface = [&](int s) -> DevSurface<T> {
         DevSurface<T> d = load_surface<T>(surf + s);
+        if ((d.rcp_ok & 16) && vac_one) d.rcp_ok |= 4 | ((d.rcp_ok & 32) ? 8 : 0);
         if constexpr (kIdx) {
             if (all_idx && !(d.rcp_ok & 4)) {
                 d.nr = lds_table[a.nkeys * (a.nsurf + 2 + s) + widx];

@@ -10,5 +10,5 @@ mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:warnings --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || exit $?
 echo pytest done
 timeout -k 10 900 python3 tools/ab_variants.py --libs "$LIBS" \
-  --configs c4:1.0,c3:1.0,c2 --modes all --rounds 7 --reps 3 > $OUT/ab.log 2>&1 || exit $?
+  --configs c4:1.0,c3:1.0,c2,c5:0.5 --modes all,final --rounds 7 --reps 3 > $OUT/ab.log 2>&1 || exit $?
 echo ab done
