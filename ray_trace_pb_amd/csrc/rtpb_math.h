@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "rtpb.h"
 
@@ -38,7 +39,8 @@ struct DevSurface {
     int32_t kind;
     int32_t rcp_ok;   // bit 0: rR, bit 1: rf usable by the shared-divisor quotients (host_rcp_ok); bit 2: nr
                       // valid; bit 3: rn2 valid and usable by the quotients; bits 4 / 5: bits 2 / 3 for a
-                      // boundary with a Vacuum side, valid where the wavelength squared is finite and nonzero
+                      // boundary with a Vacuum side, valid where the wavelength squared is finite and nonzero;
+                      // bit 6: axial geometry (kAxial, see axdot)
     T c[3];      // center
     T nrm[3];    // plane normal (flat / mirror / lens)
     T ax[3];     // input_axis
@@ -196,6 +198,40 @@ RTPB_HD bool nonneg_finite(T v) {
 template <typename T>
 RTPB_HD T np_sign(T v) {
     return v > T(0) ? T(1) : (v < T(0) ? T(-1) : (v == T(0) ? T(0) : v));
+}
+
+// ------------------------------------------------------------------ axial geometry
+// Most surfaces of real systems sit on the z axis: normal and input axis exactly (+0, +0, 1), center
+// (+0, +0, cz) (lower_surface sets kAxial then).  Their products with the 0 and 1 components are exact, so
+//   v - (+0) == v,   v * 1 == v,   RN(RN(a * 0) + b) == fma(a, 0, b)
+// bit for bit -- zero signs, infinities and NaN included (an fma rounds once, and a product that is exact
+// leaves nothing to round) -- and the reference's expressions shrink without changing a result:
+//   ((x - 0) * 0 + (y - 0) * 0) + (z - cz) * 1  ==  fma(y, 0, x * 0) + (z - cz)      (5 -> 3 float64 ops)
+// The specialised surface steps (surface_step<..., AX = true>) use only these identities.
+constexpr int32_t kAxial = 64;
+
+RTPB_HD double tfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// v . n for a surface vector n; AX: n == (+0, +0, 1)
+template <bool AX, typename T>
+RTPB_HD T axdot(T vx, T vy, T vz, T nx, T ny, T nz) {
+    if constexpr (AX) {
+        (void)nx; (void)ny; (void)nz;
+        return tfma(vy, T(0), vx * T(0)) + vz;
+    } else {
+        return vx * nx + vy * ny + vz * nz;
+    }
+}
+
+// v - c for the x / y component of a surface center; AX: c == +0
+template <bool AX, typename T>
+RTPB_HD T axsub(T v, T c) {
+    if constexpr (AX) {
+        (void)c;
+        return v;
+    } else {
+        return v - c;
+    }
 }
 
 // ------------------------------------------------------------------ shared-divisor quotients
@@ -433,11 +469,12 @@ RTPB_HD bool table_has_key(const DevMaterial<T>& m, T wl, TablePtr table) {
 // ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
 // iden: optional make_rcp of the denominator d.nrm, shared by several planes with the same normal.
-template <typename T, class G = GuardBranch>
+// AXN: the normal is (+0, +0, 1); AXC: cx and cy are +0 (axdot / axsub).
+template <bool AXN = false, bool AXC = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
                         const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr, G* g = nullptr) {
-    const T num = -((r.x - cx) * nx + (r.y - cy) * ny + (r.z - cz) * nz);
-    const T den = r.dx * nx + r.dy * ny + r.dz * nz;
+    const T num = -axdot<AXN>(axsub<AXC>(r.x, cx), axsub<AXC>(r.y, cy), r.z - cz, nx, ny, nz);
+    const T den = axdot<AXN>(r.dx, r.dy, r.dz, nx, ny, nz);
     const T t = iden ? div1_as(num, den, *iden, g) : num / den;
     const T s = t < T(0) ? T(-1) : T(1);
     const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
@@ -472,9 +509,9 @@ RTPB_HD T sphere_root(T B, T root) {
     return t;
 }
 
-template <typename T, class G = GuardBranch>
+template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr) {
-    const T ox = r.x - s.c[0], oy = r.y - s.c[1], oz = r.z - s.c[2];
+    const T ox = axsub<AX>(r.x, s.c[0]), oy = axsub<AX>(r.y, s.c[1]), oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ox * ox + oy * oy + oz * oz - s.R2;
     const T t = sphere_root(B, tsqrt<T>(B * B - T(4) * C, g));
@@ -515,15 +552,29 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 }
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
-template <typename T, class G = GuardBranch>
+// AX: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot)
+template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
-    T bx = ri.dy * Nz - ri.dz * Ny;
-    T by = ri.dz * Nx - ri.dx * Nz;
-    T bz = ri.dx * Ny - ri.dy * Nx;
+    T bx, by, bz;
+    if constexpr (AX) {
+        bx = tfma(-ri.dz, T(0), ri.dy);                   // dy * 1 - dz * 0
+        by = tfma(ri.dz, T(0), -ri.dx);                   // dz * 0 - dx * 1
+        bz = tfma(-ri.dy, T(0), ri.dx * T(0));            // dx * 0 - dy * 0
+    } else {
+        bx = ri.dy * Nz - ri.dz * Ny;
+        by = ri.dz * Nx - ri.dx * Nz;
+        bz = ri.dx * Ny - ri.dy * Nx;
+    }
     unit_or_zero(bx, by, bz, g);
-    cx = Ny * bz - Nz * by;
-    cy = Nz * bx - Nx * bz;
-    cz = Nx * by - Ny * bx;
+    if constexpr (AX) {
+        cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
+        cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
+        cz = tfma(-bx, T(0), by * T(0));                  // 0 * by - 0 * bx
+    } else {
+        cx = Ny * bz - Nz * by;
+        cy = Nz * bx - Nx * bz;
+        cz = Nx * by - Ny * bx;
+    }
     unit_or_zero(cx, cy, cz, g);
 }
 
@@ -538,16 +589,23 @@ RTPB_HD T signed_root(T v, T root) {
 
 // Snell refraction of the intersected ray (RT:1197-1221)
 // ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
-template <typename T, class G = GuardBranch>
+// AX: N == (+0, +0, 1) (axdot)
+template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
+    tangent_basis<AX>(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
-    const T tang = signed_root(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz, tsqrt<T>(T(1) - mag * mag, g));
+    const T tang = signed_root(axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz), tsqrt<T>(T(1) - mag * mag, g));
     Ray<T> o;
-    o.dx = mag * cx + tang * Nx;
-    o.dy = mag * cy + tang * Ny;
-    o.dz = mag * cz + tang * Nz;
+    if constexpr (AX) {
+        o.dx = tfma(tang, T(0), mag * cx);
+        o.dy = tfma(tang, T(0), mag * cy);
+        o.dz = mag * cz + tang;
+    } else {
+        o.dx = mag * cx + tang * Nx;
+        o.dy = mag * cy + tang * Ny;
+        o.dz = mag * cz + tang * Nz;
+    }
     o.x = ri.x; o.y = ri.y; o.z = ri.z;
     o.ph = ri.ph;
     o.wl = ri.wl;
@@ -578,22 +636,30 @@ RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
 }
 
 // FlatSurface / PlaneMirror .is_pt_on_surface (RT:1339-1347, RT:1405-1412)
-template <typename T>
+template <bool AX = false, typename T>
 RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
-    const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
-    const T h = rx * s.nrm[0] + ry * s.nrm[1] + rz * s.nrm[2];
+    const T rx = axsub<AX>(p.x, s.c[0]), ry = axsub<AX>(p.y, s.c[1]), rz = p.z - s.c[2];
+    const T h = axdot<AX>(rx, ry, rz, s.nrm[0], s.nrm[1], s.nrm[2]);
     return tabs<T>(h) < s.tol && rx * rx + ry * ry + rz * rz <= s.ap_sq;      // norm(p - c) <= aperture
 }
 
 // SphericalSurface.is_pt_on_surface (RT:1518-1535): aperture about the ORIGIN-through input axis
-template <typename T>
+// AX: axis (+0, +0, 1), center (+0, +0, cz) and a finite shell_hi.  Where `on` holds, d2 <= shell_hi < inf
+// makes p finite; then a = p.z up to a zero sign, q = (p.x -+ 0, p.y -+ 0, +-0), and the aperture sum
+// (qx qx + qy qy) + qz qz is exactly p.x p.x + p.y p.y -- the first partial sum of d2.
+template <bool AX = false, typename T>
 RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
-    const T rx = p.x - s.c[0], ry = p.y - s.c[1], rz = p.z - s.c[2];
-    const T d2 = rx * rx + ry * ry + rz * rz;
+    const T rx = axsub<AX>(p.x, s.c[0]), ry = axsub<AX>(p.y, s.c[1]), rz = p.z - s.c[2];
+    const T rxy = rx * rx + ry * ry;
+    const T d2 = rxy + rz * rz;
     const bool on = d2 >= s.shell_lo && d2 <= s.shell_hi;                      // |norm(p - c) - |R|| < tol
-    const T a = p.x * s.ax[0] + p.y * s.ax[1] + p.z * s.ax[2];
-    const T qx = p.x - a * s.ax[0], qy = p.y - a * s.ax[1], qz = p.z - a * s.ax[2];
-    return on && qx * qx + qy * qy + qz * qz <= s.ap_sq;                        // norm(ortho) <= aperture
+    if constexpr (AX) {
+        return on && rxy <= s.ap_sq;
+    } else {
+        const T a = p.x * s.ax[0] + p.y * s.ax[1] + p.z * s.ax[2];
+        const T qx = p.x - a * s.ax[0], qy = p.y - a * s.ax[1], qz = p.z - a * s.ax[2];
+        return on && qx * qx + qy * qy + qz * qz <= s.ap_sq;                    // norm(ortho) <= aperture
+    }
 }
 
 // ------------------------------------------------------------------ one surface: (at, after)
@@ -601,22 +667,31 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
 // One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
-template <typename T, int KIND, typename EmitAt, class G = GuardBranch>
+// AX: the surface has kAxial geometry (not for PLANE_MIRROR).
+template <typename T, int KIND, bool AX = false, typename EmitAt, class G = GuardBranch>
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                           Ray<T>& after, G* g = nullptr) {
     if constexpr (KIND == PERFECT_LENS) {
         const T f = s.f;
         const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
         // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
-        const Rcp<T> iden = make_rcp(r.dx * nx + r.dy * ny + r.dz * nz);
-        emit_at(to_plane(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden, g));   // RT:1790-1793
+        const Rcp<T> iden = make_rcp(axdot<AX>(r.dx, r.dy, r.dz, nx, ny, nz));
+        emit_at(to_plane<AX, AX>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
+                                 g));   // RT:1790-1793
         // (host-side F, B and n^2 f for uniform media measured 3 % slower on C4: the merged values cost
         // registers, profiles/r03/experiments/ab_lens_constants.log)
         const T Fx = s.c[0] - s.nf[0] * n1, Fy = s.c[1] - s.nf[1] * n1, Fz = s.c[2] - s.nf[2] * n1;
         const T Bx = s.c[0] + s.nf[0] * n2, By = s.c[1] + s.nf[1] * n2, Bz = s.c[2] + s.nf[2] * n2;
-        const Ray<T> rf = to_plane(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
-        const T dn = rf.dx * nx + rf.dy * ny + rf.dz * nz;
-        T spx = rf.dx - dn * nx, spy = rf.dy - dn * ny, spz = rf.dz - dn * nz;
+        const Ray<T> rf = to_plane<AX, false>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
+        const T dn = axdot<AX>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
+        T spx, spy, spz;
+        if constexpr (AX) {
+            spx = tfma(-dn, T(0), rf.dx);                 // dx - dn * 0
+            spy = tfma(-dn, T(0), rf.dy);
+            spz = rf.dz - dn;                             // dz - dn * 1
+        } else {
+            spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
+        }
         const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz, g);
         if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
         const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
@@ -638,30 +713,36 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             sin_t2 = q1 / n2;
         }
         const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
-        o.dx = sin_t2 * ux + cos_t2 * nx;
-        o.dy = sin_t2 * uy + cos_t2 * ny;
-        o.dz = sin_t2 * uz + cos_t2 * nz;
+        if constexpr (AX) {
+            o.dx = tfma(cos_t2, T(0), sin_t2 * ux);
+            o.dy = tfma(cos_t2, T(0), sin_t2 * uy);
+            o.dz = sin_t2 * uz + cos_t2;
+        } else {
+            o.dx = sin_t2 * ux + cos_t2 * nx;
+            o.dy = sin_t2 * uy + cos_t2 * ny;
+            o.dz = sin_t2 * uz + cos_t2 * nz;
+        }
         o.wl = r.wl;
         kill_if(tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a, o);
         const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
         // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
         const T k = iwl.k;
         o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
-        after = to_plane(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
-                         static_cast<const Rcp<T>*>(nullptr), g);
+        after = to_plane<AX, AX>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
+                                 static_cast<const Rcp<T>*>(nullptr), g);
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
         if constexpr (KIND == SPHERE) {
-            ri = sphere_hit(r, s, n1, iwl, g);
-            Nx = ri.x - s.c[0];                                            // (p - c) / R, RT:1476
-            Ny = ri.y - s.c[1];
+            ri = sphere_hit<AX>(r, s, n1, iwl, g);
+            Nx = axsub<AX>(ri.x, s.c[0]);                                  // (p - c) / R, RT:1476
+            Ny = axsub<AX>(ri.y, s.c[1]);
             Nz = ri.z - s.c[2];
             div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-            ri = to_plane(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
-                          static_cast<const Rcp<T>*>(nullptr), g);                  // RT:1331-1337, 1398-1403
+            ri = to_plane<AX, AX>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
+                                  static_cast<const Rcp<T>*>(nullptr), g);          // RT:1331-1337, 1398-1403
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
@@ -669,7 +750,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
-            kill_if(r.dx * s.ax[0] + r.dy * s.ax[1] + r.dz * s.ax[2] < T(0), ri);
+            kill_if(axdot<AX>(r.dx, r.dy, r.dz, s.ax[0], s.ax[1], s.ax[2]) < T(0), ri);
             emit_at(ri);
             T ratio;
             if (s.rcp_ok & 4) {
@@ -678,24 +759,45 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             } else {
                 ratio = n1 / n2;
             }
-            after = snell(ri, Nx, Ny, Nz, ratio, g);
-            const bool ok = (KIND == SPHERE) ? on_sphere(ri, s) : on_flat(ri, s);
+            after = snell<AX && KIND == FLAT>(ri, Nx, Ny, Nz, ratio, g);
+            const bool ok = (KIND == SPHERE) ? on_sphere<AX>(ri, s) : on_flat<AX>(ri, s);
             kill_if(!ok, after);
         }
     }
 }
 
-// Any surface: a wave-uniform switch on the kind.  WITH_LENS = false compiles the PerfectLens case out
-// (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans without PerfectLens
-// surfaces (rtpb_plan::feat).
+// Any surface: a wave-uniform switch on the kind (and on kAxial geometry): calls
+// step(integral_constant<int, KIND>, integral_constant<bool, AX>).  WITH_LENS = false compiles the
+// PerfectLens case out (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans
+// without PerfectLens surfaces (rtpb_plan::feat).
+template <bool WITH_LENS, typename T, typename Step>
+RTPB_HD void dispatch_kind(const DevSurface<T>& s, Step&& step) {
+    using std::integral_constant;
+    const int kind = s.kind;
+    const bool ax = (s.rcp_ok & kAxial) != 0;
+    if (WITH_LENS && kind == PERFECT_LENS) {
+        if constexpr (WITH_LENS) {
+            if (ax) step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, true>());
+            else step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, false>());
+        }
+    } else if (kind == SPHERE) {
+        if (ax) step(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
+        else step(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+    } else if (kind == PLANE_MIRROR) {
+        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<bool, false>());
+    } else if (ax) {
+        step(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+    } else {
+        step(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+    }
+}
+
 template <typename T, bool WITH_LENS = true, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
                                     EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
-    const int kind = s.kind;
-    if (WITH_LENS && kind == PERFECT_LENS) surface_step<T, PERFECT_LENS>(s, r, n1, n2, iwl, emit_at, after, g);
-    else if (kind == SPHERE) surface_step<T, SPHERE>(s, r, n1, n2, iwl, emit_at, after, g);
-    else if (kind == PLANE_MIRROR) surface_step<T, PLANE_MIRROR>(s, r, n1, n2, iwl, emit_at, after, g);
-    else surface_step<T, FLAT>(s, r, n1, n2, iwl, emit_at, after, g);
+    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
+        surface_step<T, decltype(kind)::value, decltype(ax)::value>(s, r, n1, n2, iwl, emit_at, after, g);
+    });
 }
 
 // Two independent rays through the same surface: one kind dispatch, both bodies in one straight-line
@@ -705,20 +807,12 @@ RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, co
                                     const Rcp<T>& iwl_a, const Rcp<T>& iwl_b, Ray<T>& after_a, Ray<T>& after_b,
                                     G* g = nullptr) {
     auto none = [](const Ray<T>&) {};
-    const int kind = s.kind;
-    if (WITH_LENS && kind == PERFECT_LENS) {
-        surface_step<T, PERFECT_LENS>(s, ra, n1, n2, iwl_a, none, after_a, g);
-        surface_step<T, PERFECT_LENS>(s, rb, n1, n2, iwl_b, none, after_b, g);
-    } else if (kind == SPHERE) {
-        surface_step<T, SPHERE>(s, ra, n1, n2, iwl_a, none, after_a, g);
-        surface_step<T, SPHERE>(s, rb, n1, n2, iwl_b, none, after_b, g);
-    } else if (kind == PLANE_MIRROR) {
-        surface_step<T, PLANE_MIRROR>(s, ra, n1, n2, iwl_a, none, after_a, g);
-        surface_step<T, PLANE_MIRROR>(s, rb, n1, n2, iwl_b, none, after_b, g);
-    } else {
-        surface_step<T, FLAT>(s, ra, n1, n2, iwl_a, none, after_a, g);
-        surface_step<T, FLAT>(s, rb, n1, n2, iwl_b, none, after_b, g);
-    }
+    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
+        constexpr int K = decltype(kind)::value;
+        constexpr bool A = decltype(ax)::value;
+        surface_step<T, K, A>(s, ra, n1, n2, iwl_a, none, after_a, g);
+        surface_step<T, K, A>(s, rb, n1, n2, iwl_b, none, after_b, g);
+    });
 }
 
 // R independent rays through the same surface, in place (R = 2 is propagate_surface_pair).
@@ -733,20 +827,11 @@ RTPB_HD void propagate_surface_multi(const DevSurface<T>& s, Ray<T> (&r)[R], T n
     } else {
         auto none = [](const Ray<T>&) {};
         Ray<T> o[R];
-        const int kind = s.kind;
-        if (WITH_LENS && kind == PERFECT_LENS) {
+        dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
 #pragma unroll
-            for (int q = 0; q < R; ++q) surface_step<T, PERFECT_LENS>(s, r[q], n1, n2, iwl, none, o[q], g);
-        } else if (kind == SPHERE) {
-#pragma unroll
-            for (int q = 0; q < R; ++q) surface_step<T, SPHERE>(s, r[q], n1, n2, iwl, none, o[q], g);
-        } else if (kind == PLANE_MIRROR) {
-#pragma unroll
-            for (int q = 0; q < R; ++q) surface_step<T, PLANE_MIRROR>(s, r[q], n1, n2, iwl, none, o[q], g);
-        } else {
-#pragma unroll
-            for (int q = 0; q < R; ++q) surface_step<T, FLAT>(s, r[q], n1, n2, iwl, none, o[q], g);
-        }
+            for (int q = 0; q < R; ++q)
+                surface_step<T, decltype(kind)::value, decltype(ax)::value>(s, r[q], n1, n2, iwl, none, o[q], g);
+        });
 #pragma unroll
         for (int q = 0; q < R; ++q) r[q] = o[q];
     }
@@ -829,6 +914,15 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     d.rf = 1.0 / s.focal_len;
     d.rcp_ok = (host_rcp_ok(s.radius) ? 1 : 0) | (host_rcp_ok(s.focal_len) ? 2 : 0);
     for (int j = 0; j < 3; ++j) d.nf[j] = s.normal[j] * s.focal_len;     // RT:1682-1687 `normal * focal_len`
+    // kAxial: the exact +0 / 1 components the specialised steps rely on (bit patterns: -0 does not qualify)
+    auto is_p0 = [](double v) { return host::bits(v) == 0; };
+    auto z_axis = [&](const double* v) { return is_p0(v[0]) && is_p0(v[1]) && v[2] == 1.0; };
+    const bool on_axis = is_p0(s.center[0]) && is_p0(s.center[1]);
+    bool axial = false;
+    if (d.kind == FLAT) axial = on_axis && z_axis(s.normal) && z_axis(s.input_axis);
+    else if (d.kind == SPHERE) axial = on_axis && z_axis(s.input_axis) && d.shell_hi < HUGE_VAL;
+    else if (d.kind == PERFECT_LENS) axial = on_axis && z_axis(s.normal);
+    if (axial) d.rcp_ok |= kAxial;
     d.nr = 0.0;
     d.rn2 = 0.0;
     return d;

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kTraceBlock) void plane_kernel(PlaneArgs a) {
         DevMaterial<double> m = *a.mat;
         const double n = material_n<double>(m, r.wl, a.table);
         double t;
-        const Ray<double> o = to_plane<double>(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0,
+        const Ray<double> o = to_plane(r, nv[0], nv[1], nv[2], cv[0], cv[1], cv[2], n, a.exclude != 0,
                                                   make_rcp(r.wl), &t);
         tile_write<TS>(tile, lane, o);
         if (a.ts) a.ts[i] = t;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kTraceBlock) void interact_kernel(HookArgs a) {
             const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
             const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);
             const double n2 = material_n<double>(load_material<double>(mp + 1), h.wl, a.table);
-            o = snell<double>(h, Nx, Ny, Nz, n1 / n2);                              // RT:1194-1221
+            o = snell(h, Nx, Ny, Nz, n1 / n2);                              // RT:1194-1221
         }
         if (a.on && !a.on[i]) kill(o);                                               // RT:1225-1226, 1293-1294
         tile_write<TS>(tile, lane, o);
