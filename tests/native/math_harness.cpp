@@ -77,3 +77,6 @@ extern "C" void harness_bounds(double aperture, double abs_radius, double tol, d
     out[0] = host::sqrt_le_bound(aperture);
     host::shell_bounds(abs_radius, tol, out[1], out[2]);
 }
+
+// rcp_ok flags lower_surface (rtpb_math.h) gives a surface (kAxial = 64: the axial-geometry steps)
+extern "C" int harness_surface_flags(const rtpb_surface* s) { return lower_surface(*s).rcp_ok; }

@@ -33,6 +33,15 @@ def harness():
     return _lib
 
 
+def surface_flags(low):
+    """lower_surface's rcp_ok flags of every surface of a lowered system (bit 6 = kAxial)."""
+    fn = harness().harness_surface_flags
+    fn.argtypes, fn.restype = [ctypes.c_void_p], ctypes.c_int
+    size = ctypes.sizeof(low.surfaces) // low.nsurf
+    base = ctypes.addressof(low.surfaces)
+    return [fn(base + k * size) for k in range(low.nsurf)]
+
+
 def harness_trace(low, rays2d, dtype=np.float64):
     """Full history (2S+1, N, 8) of rays2d through a lowered system (ray_trace_pb_amd._engine.lower)."""
     rays2d = np.ascontiguousarray(rays2d, dtype=dtype)
