@@ -78,6 +78,27 @@ VARIANTS = {
         "    return static_cast<uint32_t>(__builtin_amdgcn_frexp_exp(a) + 799) <= 1399u;",
         "    const uint32_t h2 = static_cast<uint32_t>(__double2hiint(a)) << 1;\n"
         "    return h2 - (223u << 21) < (1400u << 21) || __builtin_amdgcn_class(a, 0x267);")]),
+    # ray blocks in a permuted order (groups of G consecutive blocks, the group order scattered by an odd
+    # multiplier modulo the next power of two, cycle-walked into range): concurrently running waves write
+    # each history plane at scattered offsets instead of one advancing window per plane
+    **{f"perm{G}": (False, [], [(
+        "rtpb_trace_kernel.h",
+        "    body(static_cast<int64_t>(blockIdx.x));",
+        "    {\n"
+        f"        constexpr int64_t G = {G};\n"
+        "        const int64_t ng = static_cast<int64_t>(gridDim.x) / G;\n"
+        "        int64_t b = blockIdx.x;\n"
+        "        const int64_t gi = b / G;\n"
+        "        if (gi < ng) {\n"
+        "            uint64_t K = 1;\n"
+        "            while (K < static_cast<uint64_t>(ng)) K <<= 1;\n"
+        "            uint64_t y = static_cast<uint64_t>(gi);\n"
+        "            do { y = (y * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) & (K - 1); }\n"
+        "            while (y >= static_cast<uint64_t>(ng));\n"
+        "            b = static_cast<int64_t>(y) * G + (b % G);\n"
+        "        }\n"
+        "        body(b);\n"
+        "    }")]) for G in (1, 16, 256)},
     "noratio": (False, [], [(
         "rtpb_math.h",
         "            after = snell(ri, Nx, Ny, Nz, (s.rcp_ok & 4) ? s.nr : n1 / n2, g);",

@@ -18,6 +18,12 @@ step() {  # name timeout cmd...
 }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:warnings --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+# the in-tree build against the previous commit's (when tools/ built it as exp_prev.so): histories, then the C5 sweep
+if [ -f ray_trace_pb_amd/exp_prev.so ]; then
+  step ab_prev 900 python3 tools/ab_variants.py --libs ray_trace_pb_amd/exp_prev.so --configs c4:1.0,c3:1.0,c2 --modes all,final --rounds 7 --reps 3
+  step c5_new 300 python3 tools/c5_sweep.py
+  step c5_prev 300 python3 tools/c5_sweep.py --lib ray_trace_pb_amd/exp_prev.so
+fi
 step bench 900 python bench.py --steps 20 --warmup 5
 step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d $P/rocprof -o bench -- python3 bench.py --cpu-baseline off --traffic off --steps 20 --warmup 5
 step pmc_c4 900 bash tools/pmc_kernel.sh $P/pmc_c4 trace_kernel python3 tools/run_variant.py --config c4:1.0 --reps 2

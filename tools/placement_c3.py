@@ -3,7 +3,10 @@
 by a few rays (the (P, N, 8) view keeps the drop-in indexing), interleaved over rounds; plus a plain
 fill of each buffer.  A per-buffer spread that stays put across rounds is physical placement.
 
-    python tools/placement_c3.py [--buffers 4] [--pads 64,4096,65537] [--scale 1.0]
+    python tools/placement_c3.py [--buffers 4] [--pads 64,4096,65537] [--scale 1.0] [--libs a.so,b.so]
+
+--libs adds experiment builds: every (library, buffer) pair is timed, interleaved, so a change of the
+kernel's write order can be judged over several placements instead of one.
 """
 import argparse
 import collections
@@ -29,9 +32,14 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--libs", default="")
+    ap.add_argument("--sequential", action="store_true",
+                    help="buffers in allocation order, no interleaving (per-dispatch PMC attribution)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    lib = C.lib()
+    libs = {"base": C.lib()}
+    for path in [q for q in args.libs.split(",") if q]:
+        libs[os.path.basename(path).replace(".so", "")] = ab_variants.load(path)
     system, m0, m1, x, code = ab_variants.build_case(f"c3:{args.scale}", dev)
     n, S = x.shape[0], len(system.surfaces)
     low = E.lower(system.surfaces, [m0] + list(system.materials) + [m1], lambda: np.array([0.635]), code)
@@ -45,27 +53,37 @@ def main():
         b = torch.empty((P, n + pad, 8), dtype=torch.float32, device=dev)
         bufs[f"pad{pad}"] = (b, n + pad)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    plan = E.plan_for(low)
+    plans = {}
+    for ln, lib in libs.items():
+        h = ctypes.c_void_p()
+        C.check(lib.rtpb_plan_create(low.surfaces, low.nsurf, low.materials, low.nsurf + 1, low.dtype,
+                                     ctypes.byref(h)))
+        plans[ln] = h
 
-    def trace(buf, stride_rays):
-        C.check(lib.rtpb_trace(plan, 0, x.data_ptr(), C.RTPB_F64, n, C.RTPB_AOS, 0, buf.data_ptr(), C.RTPB_AOS,
-                               stride_rays * 8, 0, lo, hi, stream))
+    def trace(buf, stride_rays, ln="base"):
+        C.check(libs[ln].rtpb_trace(plans[ln], 0, x.data_ptr(), C.RTPB_F64, n, C.RTPB_AOS, 0, buf.data_ptr(),
+                                    C.RTPB_AOS, stride_rays * 8, 0, lo, hi, stream))
 
     times, fills = collections.defaultdict(list), collections.defaultdict(list)
     rng = np.random.default_rng(0)
     names = list(bufs)
+    items = [(ln, name) for ln in libs for name in names]
     for _ in range(args.rounds):
-        for name in [names[i] for i in rng.permutation(len(names))]:
+        order = range(len(items)) if args.sequential else rng.permutation(len(items))
+        for ln, name in [items[i] for i in order]:
             buf, stride = bufs[name]
-            trace(buf, stride)
+            lib = libs[ln]
+            trace(buf, stride, ln)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
             for _ in range(args.reps):
-                trace(buf, stride)
+                trace(buf, stride, ln)
             tot, cnt = ctypes.c_double(), ctypes.c_int64()
             C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
             lib.rtpb_timing_enable(0)
-            times[name].append(tot.value / cnt.value)
+            times[(ln, name)].append(tot.value / cnt.value)
+            if ln != "base":
+                continue
             flat = buf.view(-1)
             chunks = [flat[k:k + (1 << 30)] for k in range(0, flat.numel(), 1 << 30)]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,20 +93,28 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             fills[name].append(flat.numel() * 4 / (e0.elapsed_time(e1) * 1e-3) / 1e9)
-    # every padded / separately allocated trace gives the same history (compare against plain0)
+    # every library / padded / separately allocated trace gives the same history (compare against plain0)
     ref, _ = bufs["plain0"]
     trace(ref, n)
+    torch.cuda.synchronize()
+    ref = ref.clone()
     res = {"rays": n, "planes": P, "alg_bytes": n * (64 + 32 * P)}
-    for name in names:
-        buf, stride = bufs[name]
-        trace(buf, stride)
-        torch.cuda.synchronize()
-        same = all(bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) for a, b in zip(ref, buf[:, :n]))
-        ms = float(np.median(times[name]))
-        res[name] = {"ms": ms, "ms_all": [round(t, 4) for t in times[name]], "alg_GBps": res["alg_bytes"] / ms / 1e6,
-                     "fill_GBps": float(np.median(fills[name])), "identical": same}
-        print(f"{name:10s} ms={ms:.4f} ({', '.join(f'{t:.3f}' for t in times[name])}) "
-              f"{res['alg_bytes'] / ms / 1e6:.0f} GB/s  fill {np.median(fills[name]):.0f} GB/s  same={same}", flush=True)
+    for ln in libs:
+        for name in names:
+            buf, stride = bufs[name]
+            trace(buf, stride, ln)
+            torch.cuda.synchronize()
+            same = all(bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) for a, b in zip(ref, buf[:, :n]))
+            ms = float(np.median(times[(ln, name)]))
+            res[f"{ln}:{name}"] = {"ms": ms, "ms_all": [round(t, 4) for t in times[(ln, name)]],
+                                   "alg_GBps": res["alg_bytes"] / ms / 1e6,
+                                   "fill_GBps": float(np.median(fills[name])), "identical": same}
+            print(f"{ln:12s} {name:10s} ms={ms:.4f} ({', '.join(f'{t:.3f}' for t in times[(ln, name)])}) "
+                  f"{res['alg_bytes'] / ms / 1e6:.0f} GB/s  fill {np.median(fills[name]):.0f} GB/s  same={same}",
+                  flush=True)
+        ms = [res[f"{ln}:{name}"]["ms"] for name in names]
+        print(f"{ln:12s} over buffers: min {min(ms):.4f} median {float(np.median(ms)):.4f} max {max(ms):.4f} ms",
+              flush=True)
     print(json.dumps(res))
 
 
