@@ -99,6 +99,10 @@ VARIANTS = {
         "        }\n"
         "        body(b);\n"
         "    }")]) for G in (1, 16, 256)},
+    # cache policy of the history stores (gfx950 cpol: sc0 = 1, nt = 2, sc1 = 16; shipped: nt | sc1)
+    **{f"pol{v}": (False, [], [(
+        "rtpb_internal.h", "constexpr int kAux = NT ? (2 | 16) : 0;", f"constexpr int kAux = NT ? {v} : 0;")])
+       for v in (2, 3, 19, 17)},
     "noratio": (False, [], [(
         "rtpb_math.h",
         "            after = snell(ri, Nx, Ny, Nz, (s.rcp_ok & 4) ? s.nr : n1 / n2, g);",
