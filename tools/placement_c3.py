@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--libs", default="")
+    ap.add_argument("--rays-copy", action="store_true",
+                    help="also trace from a copy of the input rays allocated after the buffers")
     ap.add_argument("--sequential", action="store_true",
                     help="buffers in allocation order, no interleaving (per-dispatch PMC attribution)")
     args = ap.parse_args()
@@ -53,6 +55,9 @@ def main():
         b = torch.empty((P, n + pad, 8), dtype=torch.float32, device=dev)
         bufs[f"pad{pad}"] = (b, n + pad)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    inputs = {"": x}
+    if args.rays_copy:
+        inputs["@rays2"] = x.clone()
     plans = {}
     for ln, lib in libs.items():
         h = ctypes.c_void_p()
@@ -60,29 +65,31 @@ def main():
                                      ctypes.byref(h)))
         plans[ln] = h
 
-    def trace(buf, stride_rays, ln="base"):
-        C.check(libs[ln].rtpb_trace(plans[ln], 0, x.data_ptr(), C.RTPB_F64, n, C.RTPB_AOS, 0, buf.data_ptr(),
+    def trace(buf, stride_rays, ln="base", xin=x):
+        C.check(libs[ln].rtpb_trace(plans[ln], 0, xin.data_ptr(), C.RTPB_F64, n, C.RTPB_AOS, 0, buf.data_ptr(),
                                     C.RTPB_AOS, stride_rays * 8, 0, lo, hi, stream))
 
     times, fills = collections.defaultdict(list), collections.defaultdict(list)
     rng = np.random.default_rng(0)
     names = list(bufs)
-    items = [(ln, name) for ln in libs for name in names]
+    items = [(ln + xs, name) for ln in libs for xs in inputs for name in names]
     for _ in range(args.rounds):
         order = range(len(items)) if args.sequential else rng.permutation(len(items))
-        for ln, name in [items[i] for i in order]:
+        for lnx, name in [items[i] for i in order]:
+            ln, _, xs = lnx.partition("@")
+            xin = inputs["@" + xs] if xs else x
             buf, stride = bufs[name]
             lib = libs[ln]
-            trace(buf, stride, ln)
+            trace(buf, stride, ln, xin)
             torch.cuda.synchronize()
             lib.rtpb_timing_enable(1)
             for _ in range(args.reps):
-                trace(buf, stride, ln)
+                trace(buf, stride, ln, xin)
             tot, cnt = ctypes.c_double(), ctypes.c_int64()
             C.check(lib.rtpb_timing_collect(ctypes.byref(tot), ctypes.byref(cnt)))
             lib.rtpb_timing_enable(0)
-            times[(ln, name)].append(tot.value / cnt.value)
-            if ln != "base":
+            times[(lnx, name)].append(tot.value / cnt.value)
+            if lnx != "base":
                 continue
             flat = buf.view(-1)
             chunks = [flat[k:k + (1 << 30)] for k in range(0, flat.numel(), 1 << 30)]
@@ -99,21 +106,22 @@ def main():
     torch.cuda.synchronize()
     ref = ref.clone()
     res = {"rays": n, "planes": P, "alg_bytes": n * (64 + 32 * P)}
-    for ln in libs:
+    for lnx in dict.fromkeys(i[0] for i in items):
+        ln = lnx.partition("@")[0]
         for name in names:
             buf, stride = bufs[name]
             trace(buf, stride, ln)
             torch.cuda.synchronize()
             same = all(bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) for a, b in zip(ref, buf[:, :n]))
-            ms = float(np.median(times[(ln, name)]))
-            res[f"{ln}:{name}"] = {"ms": ms, "ms_all": [round(t, 4) for t in times[(ln, name)]],
+            ms = float(np.median(times[(lnx, name)]))
+            res[f"{lnx}:{name}"] = {"ms": ms, "ms_all": [round(t, 4) for t in times[(lnx, name)]],
                                    "alg_GBps": res["alg_bytes"] / ms / 1e6,
                                    "fill_GBps": float(np.median(fills[name])), "identical": same}
-            print(f"{ln:12s} {name:10s} ms={ms:.4f} ({', '.join(f'{t:.3f}' for t in times[(ln, name)])}) "
+            print(f"{lnx:12s} {name:10s} ms={ms:.4f} ({', '.join(f'{t:.3f}' for t in times[(lnx, name)])}) "
                   f"{res['alg_bytes'] / ms / 1e6:.0f} GB/s  fill {np.median(fills[name]):.0f} GB/s  same={same}",
                   flush=True)
-        ms = [res[f"{ln}:{name}"]["ms"] for name in names]
-        print(f"{ln:12s} over buffers: min {min(ms):.4f} median {float(np.median(ms)):.4f} max {max(ms):.4f} ms",
+        ms = [res[f"{lnx}:{name}"]["ms"] for name in names]
+        print(f"{lnx:12s} over buffers: min {min(ms):.4f} median {float(np.median(ms)):.4f} max {max(ms):.4f} ms",
               flush=True)
     print(json.dumps(res))
 
