@@ -142,8 +142,10 @@ class Workload:
         self.low = E.lower(self.system.surfaces, mats, lambda: wl_keys, self.code)
         self.planes = E.resolve_planes("all", self.S)
         w = 8 if self.code == C.RTPB_F64 else 4
-        self.out = torch.empty((len(self.planes), self.n, 8), dtype=torch.float64 if w == 8 else torch.float32,
-                               device=dev)
+        # the history: the product's placement-robust buffer (raytrace.history_buffer / rtpb_buffer_alloc,
+        # the out= of repeated traces), so the rate does not depend on where this process's first large
+        # allocation lands; second_buffer() times a default torch allocation beside it
+        self.out = E.history_buffer((len(self.planes), self.n, 8), torch.float64 if w == 8 else torch.float32, dev)
         self.stream = torch.cuda.current_stream(dev).cuda_stream
         # algorithmic bytes per launch, SURVEY.md §8(d) / BASELINE.md: 16 w (S+1) per ray for the full history
         # (one read of an input record and one write of each of the 2S+1 planes at the storage width w)
@@ -169,6 +171,21 @@ class Workload:
         ev1.record()
         torch.cuda.synchronize()
         return ev0.elapsed_time(ev1) / steps, time.perf_counter() - t0
+
+    def second_buffer(self, steps):
+        """Average launch duration (ms) of the same trace into a history allocated by torch's default
+        allocator (what System.ray_trace allocates without out=): the many-plane write pattern runs at a
+        rate that depends on where that memory lies (placement), so the line shows it beside
+        the timed history buffer."""
+        import torch
+        main_out = self.out
+        self.out = torch.empty(main_out.shape, dtype=main_out.dtype, device=main_out.device)
+        try:
+            self.step()
+            kernel_ms, _ = self.timed(steps)
+        finally:
+            self.out = main_out
+        return kernel_ms
 
     def e2e(self, reps=5):
         """The drop-in call on device-resident rays: System.ray_trace(torch rays, m0, m1, dtype) -- lowering,
@@ -608,6 +625,7 @@ def main():
     kernel_ms, elapsed = wl.timed(args.steps)
     _barrier(world)
     fill = wl.fill_rate() if rank == 0 else None
+    alt_ms = wl.second_buffer(args.steps) if (world == 1 and args.config in ("c3", "c2")) else None
     e2e_ms, e2e_kernel_ms = wl.e2e() if args.config == "c3" else (None, None)
     g = _gather(world, [elapsed, kernel_ms])
     per_rank = [{"rank": r, "kernel_ms": x[1], "alg_GBps": wl.alg_bytes / (x[1] * 1e-3) / 1e9, "wall_s": x[0]}
@@ -655,6 +673,13 @@ def main():
                                 "drop-in call. Interleaved with the loop's launches the call's kernel takes the "
                                 "loop's time (tools/e2e_kernel_diff.py), so e2e_over_loop_kernel also carries "
                                 "the run-to-run drift between the two measurements")
+        if alt_ms is not None:
+            line["placement_check"] = {
+                "kernel_ms_history_buffer": kernel_ms, "kernel_ms_torch_empty": alt_ms,
+                "note": "value: the trace into raytrace.history_buffer (rtpb_buffer_alloc: physical chunks mapped "
+                        "in shuffled order, the product's out= buffer for repeated traces); kernel_ms_torch_empty: "
+                        "the same launches into a torch.empty history (the default allocation of System.ray_trace "
+                        "without out=), whose many-plane write rate depends on where it lands (DESIGN.md 5)"}
         if world > 1:
             line["per_rank"] = per_rank
     del head

@@ -39,9 +39,10 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 4   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+#define RTPB_ABI_VERSION 5   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
                                 3: input element type separate from the storage type (in_dtype)
-                                4: + rtpb_trace_checked (table-miss flag) */
+                                4: + rtpb_trace_checked (table-miss flag)
+                                5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -114,6 +115,23 @@ const char* rtpb_last_error(void);
 int rtpb_device_count(void);
 /* Release every device resource the library holds (plans must be destroyed first). */
 int rtpb_shutdown(void);
+
+/* ---- history buffers (ABI 5) ------------------------------------------------------------------ */
+/* Output buffers for large histories.  The 2S+1 planes of a history are written concurrently, and that
+   write pattern runs 15-45 % slower into some physical placements -- physically contiguous memory in
+   particular, which the first large allocations of a process on an unfragmented card often are -- while a
+   plain fill of the same memory does not.  rtpb_buffer_alloc maps the buffer's physical
+   memory in `chunk_bytes` chunks (0: 64 MiB) placed in the virtual range in a shuffled order (`seed`), so
+   every buffer gets the fast rate.  The buffer is device memory like any other (pass `*ptr` to rtpb_trace).
+   rtpb_buffer_free synchronises the device (no kernel may still write to it) and releases it.
+   rtpb_buffer_dlpack wraps the whole buffer as a C-contiguous DLPack (v0.8 DLManagedTensor, device type
+   ROCm) tensor of `ndim` extents `shape` and element type `dtype` (RTPB_F64 / RTPB_F32); ownership passes
+   to the importer, whose call of the managed tensor's deleter frees the buffer.  Replaces nothing in the
+   reference (NumPy allocates its histories itself, RT:1229-1232). */
+int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void** ptr,
+                      void** handle);
+int rtpb_buffer_free(void* handle);
+int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed);
 
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
 /* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,

@@ -11,13 +11,14 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 4
+RTPB_ABI_VERSION = 5
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
 RTPB_FLAT, RTPB_SPHERE, RTPB_PLANE_MIRROR, RTPB_PERFECT_LENS = 0, 1, 2, 3
 RTPB_CONSTANT, RTPB_SELLMEIER, RTPB_POLY6, RTPB_TABLE = 0, 1, 2, 3
 RTPB_MAX_SURFACES = 63
+RTPB_OK, RTPB_E_INVALID, RTPB_E_HIP, RTPB_E_NODEV, RTPB_E_LIMIT = 0, -1, -2, -3, -4
 
 _c3 = ctypes.c_double * 3
 _c6 = ctypes.c_double * 6
@@ -52,6 +53,9 @@ SIGNATURES = {
     "rtpb_last_error": (ctypes.c_char_p, []),
     "rtpb_device_count": (ctypes.c_int, []),
     "rtpb_shutdown": (ctypes.c_int, []),
+    "rtpb_buffer_alloc": (ctypes.c_int, [_i32, _u64, _u64, _u64, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "rtpb_buffer_free": (ctypes.c_int, [_P]),
+    "rtpb_buffer_dlpack": (ctypes.c_int, [_P, _i32, ctypes.POINTER(_i64), _i32, ctypes.POINTER(_P)]),
     "rtpb_plan_create": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _i32,
                                         ctypes.POINTER(_P)]),
     "rtpb_plan_destroy": (ctypes.c_int, [_P]),

@@ -13,6 +13,7 @@
 import collections
 import contextlib
 import ctypes
+import itertools
 import threading
 
 import numpy as np
@@ -417,6 +418,58 @@ def trace_host(low, rays2d, planes, devices=None, out=None):
         ndev = len(devices)
     with plan_ref(low) as plan:
         C.check(C.lib().rtpb_trace_host(plan, rays2d.ctypes.data, in_code, n, out.ctypes.data, lo, hi, devs, ndev))
+    return out
+
+
+_DLTENSOR = b"dltensor"
+_buffer_seed = itertools.count(1)
+
+
+def history_buffer(shape, dtype, device, chunk_bytes=0):
+    """A C-contiguous torch CUDA tensor of ``shape`` and ``dtype`` (float32 / float64) on ``device`` whose
+    memory comes from rtpb_buffer_alloc: physical chunks (64 MiB) mapped in a shuffled order, so a history
+    traced into it writes at the fast rate whatever the physical state of the card (a history's many-plane
+    write pattern runs 15-45 % slower into physically contiguous placements).  Use it for the
+    ``out=`` of repeated traces; freeing it synchronises its device."""
+    import torch
+    if dtype not in (torch.float32, torch.float64):
+        raise ValueError("history_buffer: dtype must be torch.float32 or torch.float64")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError("history_buffer: a CUDA (HIP) device is required")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    shape = tuple(int(v) for v in shape)
+    elem = 8 if dtype == torch.float64 else 4
+    nbytes = elem
+    for v in shape:
+        nbytes *= v
+    if nbytes == 0:
+        return torch.empty(shape, dtype=dtype, device=dev)
+    lib = C.lib()
+    ptr, handle = ctypes.c_void_p(), ctypes.c_void_p()
+    C.check(lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, next(_buffer_seed), ctypes.byref(ptr),
+                                  ctypes.byref(handle)))
+    managed = ctypes.c_void_p()
+    ext = (ctypes.c_int64 * len(shape))(*shape)
+    rc = lib.rtpb_buffer_dlpack(handle, len(shape), ext, C.RTPB_F64 if elem == 8 else C.RTPB_F32,
+                                ctypes.byref(managed))
+    if rc != 0:
+        lib.rtpb_buffer_free(handle)
+        C.check(rc)
+    new_capsule = ctypes.pythonapi.PyCapsule_New
+    new_capsule.restype = ctypes.py_object
+    new_capsule.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    return torch.utils.dlpack.from_dlpack(new_capsule(managed, _DLTENSOR, None))
+
+
+def check_out(out, shape, dtype, device):
+    """The caller's ``out=`` history: a C-contiguous CUDA tensor of exactly the history's shape and type."""
+    import torch
+    if not isinstance(out, torch.Tensor) or not out.is_cuda:
+        raise ValueError("out must be a torch CUDA tensor (e.g. ray_trace_pb_amd.raytrace.history_buffer)")
+    if tuple(out.shape) != tuple(shape) or out.dtype != dtype or out.device != device or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous {dtype} tensor of shape {tuple(shape)} on {device}; got "
+                         f"{out.dtype} {tuple(out.shape)} on {out.device}")
     return out
 
 

@@ -345,7 +345,16 @@ def shard_bounds(n, n_shards):
     return [(n * g // n_shards, n * (g + 1) // n_shards) for g in range(n_shards)]
 
 
-def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devices=None, layout="aos", gather=True):
+def history_buffer(shape, dtype, device):
+    """A preallocated history for ``ray_trace(..., out=)``: a C-contiguous torch CUDA tensor of ``shape``
+    ((P, N, 8), P stored planes) and ``dtype`` (torch.float32 / torch.float64) on ``device``, whose device
+    memory is mapped in shuffled 64 MiB chunks (rtpb_buffer_alloc) so that the history's many-plane writes
+    run at their fast rate wherever the memory lies."""
+    return E.history_buffer(shape, dtype, device)
+
+
+def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devices=None, layout="aos", gather=True,
+                   out=None):
     """Trace ``rays`` through ``surfaces`` with ``materials`` (len(surfaces)+1 entries) on the GPU.
 
     ``rays`` follows the reference's rank convention (RT:1175-1178): (8,) -> one ray, (N, 8) -> a
@@ -358,9 +367,18 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     listed GPUs, traced there concurrently, and gathered back onto its own device (``gather=False``:
     the list of per-device histories instead); a list of torch CUDA shards (one per device, e.g. from
     ``get_ray_fan(..., devices=)``) is traced where it lives and returns the list of per-device
-    histories.  Systems longer than RTPB_MAX_SURFACES run as consecutive fused segments."""
+    histories.  Systems longer than RTPB_MAX_SURFACES run as consecutive fused segments.
+
+    ``out``: a torch CUDA (N, 8) bundle on one device may be traced into a caller-provided history --
+    a C-contiguous tensor of exactly the result's shape, type and device (for example a
+    :func:`history_buffer`, whose placement keeps the many-plane writes at their fast rate); the
+    result is ``out`` itself."""
     if len(materials) != len(surfaces) + 1:
         raise ValueError("length of materials should be len(surfaces) + 1")
+    if out is not None and (not _is_torch_cuda(rays) or rays.ndim == 3 or devices is not None
+                            or len(surfaces) > C.RTPB_MAX_SURFACES):
+        raise ValueError("out= is for a torch CUDA (N, 8) or (8,) bundle on one device, up to "
+                         f"{C.RTPB_MAX_SURFACES} surfaces")
     if not surfaces:
         return rays
     if _is_shard_list(rays):
@@ -390,7 +408,7 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
 
     layout_code = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
     if on_device:
-        return _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code)
+        return _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out)
 
     def wavelengths():
         return E.distinct_wavelengths(last[:, 7])
@@ -407,7 +425,7 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     return E.trace_host(low, last, sel, devs)
 
 
-def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code):
+def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out=None):
     """The torch-CUDA trace of trace_surfaces.  Tabulated materials (user n() overrides, Ebaf11) are
     lowered with the key set of the previous bundle traced through them when there is one, and the kernel
     flags any ray whose wavelength is not among those keys (rtpb_trace_checked); only then is the bundle's
@@ -415,12 +433,16 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layou
     way every ray reads n() of its own wavelength: bit-identical to lowering with the bundle's keys."""
     import torch
     k = rays.shape[0]
+    if out is not None:
+        n = last.shape[0]
+        shape = (len(sel), n, 8) if layout_code == C.RTPB_AOS else (len(sel), 8, n)
+        E.check_out(out, shape, torch.float64 if code == C.RTPB_F64 else torch.float32, last.device)
 
     def run(low, miss=None):
         if full and k > 1:
             new = E.trace_device(low, last, sel[1:], miss=miss)
             return torch.cat((rays.to(new.dtype), new), dim=0)
-        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss)
+        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=out)
 
     tab = E.tabulated(materials)
     if not tab:
@@ -429,10 +451,10 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layou
     prev = E.previous_keys(fp)
     if prev is not None:
         miss = torch.zeros(1, dtype=torch.int32, device=last.device)
-        out = run(E.lower(surfaces, materials, lambda: prev, code), miss)
+        res = run(E.lower(surfaces, materials, lambda: prev, code), miss)
         if int(miss.item()) == 0:
-            return out
-        del out
+            return res
+        del res
     keys = E.distinct_wavelengths(last[:, 7])
     E.remember_keys(fp, keys)
     return run(E.lower(surfaces, materials, lambda: keys, code))
@@ -682,7 +704,7 @@ class System:
 
     # ------------------------------------------------------------------ the hot path (RT:641-661)
     def ray_trace(self, rays, initial_material: Material, final_material: Material, *, planes="all",
-                  dtype=None, devices=None, layout="aos", gather=True):
+                  dtype=None, devices=None, layout="aos", gather=True, out=None):
         """Trace rays through the system; returns the ray history.
 
         Same contract as the reference: (N, 8) rays -> (2S+1, N, 8) history (plane 0 = input, plane
@@ -698,6 +720,8 @@ class System:
                  scatter and gather)
         layout   'aos' (default) | 'soa' (torch inputs only: (planes, 8, N) output)
         gather   torch input with devices: False returns the list of per-device histories (no gather)
+        out      torch input on one device: trace into this preallocated history (e.g. history_buffer(...),
+                 for repeated traces) and return it
 
         torch CUDA tensors in -> torch CUDA tensors out (nothing leaves HBM); a list of per-device torch
         shards (e.g. ``get_ray_fan(..., devices=...)``) -> the list of per-device histories."""
@@ -707,7 +731,9 @@ class System:
         custom = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
-                                  layout=layout, gather=gather)
+                                  layout=layout, gather=gather, out=out)
+        if out is not None:
+            raise ValueError("out= is not available for systems with user-defined surfaces")
         # user surfaces (own propagate, or own geometry hooks): run maximal runs of built-in surfaces
         # as fused GPU traces and hand the growing history to each user surface in between
         # (RT:658-659 order)
