@@ -52,6 +52,12 @@ C4_FAN = (10001, 10000)        # scripts/2022_01_25_ray_trace_ideal_opm.py:59-92
 C5_FAN = (3163, 3162)          # scripts/2021_10_06_ray_trace_system.py:186 (10M rays per group)
 
 
+def _trim_buffers():
+    """Release the memory of freed history buffers (ray_trace_pb_amd's buffer pool) with torch's cache."""
+    from ray_trace_pb_amd import _engine as E
+    E.trim_history_buffers()
+
+
 def _log(msg):
     """Progress on stderr (the JSON line alone goes to stdout)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -252,6 +258,7 @@ def stream_copy_rate(device, nbytes=4 << 30, reps=10):
     rate = 2 * nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
     del src, dst
     torch.cuda.empty_cache()
+    _trim_buffers()
     return rate
 
 
@@ -476,6 +483,7 @@ def run_c2(args, dev, copy):
     res["host_e2e"] = host_e2e(w2)
     del w2
     torch.cuda.empty_cache()
+    _trim_buffers()
     return res
 
 
@@ -512,6 +520,7 @@ def run_c4(args, dev, rank, world, copy):
             res["roofline"]["note"] = "N=1: the whole 100M-ray fan on one GPU (80 GB in HBM)"
     del wl
     torch.cuda.empty_cache()
+    _trim_buffers()
     return res
 
 
@@ -638,6 +647,7 @@ def main():
     head = wl
     del wl
     torch.cuda.empty_cache()
+    _trim_buffers()
     copy = stream_copy_rate(dev) if rank == 0 else None
 
     line = None

@@ -123,7 +123,10 @@ int rtpb_shutdown(void);
    plain fill of the same memory does not.  rtpb_buffer_alloc maps the buffer's physical
    memory in `chunk_bytes` chunks (0: 64 MiB) placed in the virtual range in a shuffled order (`seed`), so
    every buffer gets the fast rate.  The buffer is device memory like any other (pass `*ptr` to rtpb_trace).
-   rtpb_buffer_free synchronises the device (no kernel may still write to it) and releases it.
+   rtpb_buffer_free synchronises the device (no kernel may still use the buffer) and keeps the buffer,
+   still mapped, in a pool: the next rtpb_buffer_alloc of the same size on that device returns it again
+   (a virtual range is never unmapped and mapped anew).  rtpb_buffer_trim -- and rtpb_shutdown, and an
+   allocation that finds the device full -- releases the physical memory of every pooled buffer.
    rtpb_buffer_dlpack wraps the whole buffer as a C-contiguous DLPack (v0.8 DLManagedTensor, device type
    ROCm) tensor of `ndim` extents `shape` and element type `dtype` (RTPB_F64 / RTPB_F32); ownership passes
    to the importer, whose call of the managed tensor's deleter frees the buffer.  Replaces nothing in the
@@ -131,6 +134,7 @@ int rtpb_shutdown(void);
 int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void** ptr,
                       void** handle);
 int rtpb_buffer_free(void* handle);
+int rtpb_buffer_trim(void);
 int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed);
 
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */

@@ -55,6 +55,7 @@ SIGNATURES = {
     "rtpb_shutdown": (ctypes.c_int, []),
     "rtpb_buffer_alloc": (ctypes.c_int, [_i32, _u64, _u64, _u64, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "rtpb_buffer_free": (ctypes.c_int, [_P]),
+    "rtpb_buffer_trim": (ctypes.c_int, []),
     "rtpb_buffer_dlpack": (ctypes.c_int, [_P, _i32, ctypes.POINTER(_i64), _i32, ctypes.POINTER(_P)]),
     "rtpb_plan_create": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _i32,
                                         ctypes.POINTER(_P)]),

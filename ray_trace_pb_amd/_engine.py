@@ -462,6 +462,12 @@ def history_buffer(shape, dtype, device, chunk_bytes=0):
     return torch.utils.dlpack.from_dlpack(new_capsule(managed, _DLTENSOR, None))
 
 
+def trim_history_buffers():
+    """Release the device memory of every freed history_buffer (the library keeps freed ones mapped for
+    reuse by the next buffer of the same size; rtpb_buffer_trim)."""
+    C.check(C.lib().rtpb_buffer_trim())
+
+
 def check_out(out, shape, dtype, device):
     """The caller's ``out=`` history: a C-contiguous CUDA tensor of exactly the history's shape and type."""
     import torch

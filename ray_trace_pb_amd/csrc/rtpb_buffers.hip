@@ -10,11 +10,16 @@
 // the state of VRAM: every such buffer measured at the fast rate.
 //
 // Lifetime: the caller frees a buffer with rtpb_buffer_free, or hands it to a DLPack importer
-// (rtpb_buffer_dlpack) whose deleter frees it.  Freeing synchronises the device first -- the memory is
-// unmapped, so no kernel may still be writing to it.
+// (rtpb_buffer_dlpack) whose deleter frees it.  A freed buffer is kept, still mapped, in a per-process pool
+// and handed out again to the next allocation of the same size on the same device (after the device was
+// synchronised, so no kernel still uses it); a virtual range is never unmapped and then mapped again.
+// rtpb_buffer_trim (and rtpb_shutdown) releases the physical memory of every pooled buffer; its virtual range
+// stays reserved and unused, so no translation cached by the GPU can ever point a new buffer at released
+// memory.
 #include "rtpb_internal.h"
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 using namespace rtpbi;
@@ -29,16 +34,56 @@ struct Buffer {
     std::vector<uint64_t> mapped;                          // virtual slot of each mapped chunk
 };
 
-int release(Buffer* b) {
+// Unmaps and releases the physical chunks of a buffer no one uses; its virtual range stays reserved (never
+// reused), the Buffer object is deleted.
+int destroy(Buffer* b) {
     DeviceGuard g(b->dev);
-    hipError_t e = hipDeviceSynchronize();         // nothing may still write into memory about to be unmapped
+    hipError_t e = hipDeviceSynchronize();
     for (uint64_t s : b->mapped)
         if (hipMemUnmap(static_cast<char*>(b->va) + s * b->chunk, b->chunk) != hipSuccess) e = hipErrorUnknown;
     for (auto h : b->chunks)
         if (hipMemRelease(h) != hipSuccess) e = hipErrorUnknown;
-    if (b->va && hipMemAddressFree(b->va, b->size) != hipSuccess) e = hipErrorUnknown;
     delete b;
-    return e == hipSuccess ? RTPB_OK : fail(RTPB_E_HIP, "rtpb_buffer_free: releasing the mapping failed");
+    return e == hipSuccess ? RTPB_OK : fail(RTPB_E_HIP, "rtpb_buffer: releasing a mapping failed");
+}
+
+std::mutex g_pool_mu;
+std::vector<Buffer*> g_pool;                       // freed buffers, still mapped, ready for reuse
+
+// Back to the pool once the device has finished every kernel that may use it.
+int release(Buffer* b) {
+    {
+        DeviceGuard g(b->dev);
+        if (hipDeviceSynchronize() != hipSuccess)
+            return fail(RTPB_E_HIP, "rtpb_buffer_free: hipDeviceSynchronize failed");
+    }
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back(b);
+    return RTPB_OK;
+}
+
+Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t k = 0; k < g_pool.size(); ++k) {
+        Buffer* b = g_pool[k];
+        if (b->dev == dev && b->size == size && b->chunk == chunk) {
+            g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(k));
+            return b;
+        }
+    }
+    return nullptr;
+}
+
+int trim_pool() {
+    std::vector<Buffer*> all;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        all.swap(g_pool);
+    }
+    int rc = RTPB_OK;
+    for (Buffer* b : all)
+        if (destroy(b) != RTPB_OK) rc = RTPB_E_HIP;
+    return rc;
 }
 
 // splitmix64: the shuffle's generator
@@ -102,6 +147,11 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     // a buffer smaller than one chunk is a single chunk of its own (rounded) size
     const uint64_t chunk = round_up(std::min<uint64_t>(want, round_up(bytes, gran)), gran);
     const uint64_t n = (bytes + chunk - 1) / chunk;
+    if (Buffer* p = take_pooled(device, n * chunk, chunk)) {
+        *ptr = p->va;
+        *handle = p;
+        return RTPB_OK;
+    }
     auto* b = new Buffer;
     b->dev = device;
     b->size = n * chunk;
@@ -111,7 +161,7 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     const uint64_t align = (chunk & (chunk - 1)) == 0 ? chunk : gran;
     if (hipMemAddressReserve(&b->va, b->size, align, nullptr, 0) != hipSuccess) {
         b->va = nullptr;
-        (void)release(b);
+        (void)destroy(b);
         return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemAddressReserve failed");
     }
     std::vector<uint64_t> slot(n);
@@ -123,12 +173,15 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     for (uint64_t k = 0; k < n; ++k) {
         hipMemGenericAllocationHandle_t h;
         if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
-            (void)release(b);
-            return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemCreate failed (out of device memory?)");
+            // out of memory: release the pooled buffers' memory once and retry
+            if (trim_pool() != RTPB_OK || hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+                (void)destroy(b);
+                return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemCreate failed (out of device memory?)");
+            }
         }
         b->chunks.push_back(h);
         if (hipMemMap(static_cast<char*>(b->va) + slot[k] * chunk, chunk, 0, h, 0) != hipSuccess) {
-            (void)release(b);
+            (void)destroy(b);
             return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemMap failed");
         }
         b->mapped.push_back(slot[k]);
@@ -137,7 +190,7 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;
     if (hipMemSetAccess(b->va, b->size, &acc, 1) != hipSuccess) {
-        (void)release(b);
+        (void)destroy(b);
         return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemSetAccess failed");
     }
     *ptr = b->va;
@@ -149,6 +202,8 @@ extern "C" int rtpb_buffer_free(void* handle) {
     if (!handle) return fail(RTPB_E_INVALID, "rtpb_buffer_free: null handle");
     return release(static_cast<Buffer*>(handle));
 }
+
+extern "C" int rtpb_buffer_trim(void) { return trim_pool(); }
 
 extern "C" int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed) {
     if (!handle || !managed || ndim < 1 || ndim > 8 || !shape)

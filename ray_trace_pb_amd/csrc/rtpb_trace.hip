@@ -223,6 +223,7 @@ int host_shard_pipeline(rtpb_plan* plan, int dev, const char* in, int in_dtype, 
 extern "C" {
 
 int rtpb_shutdown(void) {
+    (void)rtpb_buffer_trim();                      // pooled history buffers (rtpb_buffers.hip)
     for (int d = 0; d < kMaxDevices; ++d) {
         HostStage& hs = g_stage[d];
         std::lock_guard<std::mutex> lk(hs.mu);

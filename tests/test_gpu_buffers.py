@@ -67,15 +67,21 @@ def test_out_validation():
         system.ray_trace(x[None], m0, m1, out=torch.empty(ref.shape, dtype=torch.float64, device=DEV))
 
 
-def test_buffers_are_released():
+def test_buffers_are_pooled_and_trimmed():
+    C.check(C.lib().rtpb_buffer_trim())
     torch.cuda.synchronize()
     free0 = torch.cuda.mem_get_info()[0]
+    ptrs = set()
     for _ in range(4):
         t = rt.history_buffer((19, 50_000_000, 8), torch.float32, DEV)      # 30.4 GB: one C3 history
         t[-1, -1].fill_(1.0)
+        ptrs.add(t.data_ptr())
         del t
         gc.collect()
+    assert len(ptrs) == 1                                                   # the pooled buffer came back
     torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info()[0] < free0 - (30 << 30)                # ... and is still held
+    C.check(C.lib().rtpb_buffer_trim())
     assert torch.cuda.mem_get_info()[0] >= free0 - (256 << 20)
 
 
