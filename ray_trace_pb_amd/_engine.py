@@ -459,7 +459,11 @@ def history_buffer(shape, dtype, device, chunk_bytes=0):
     new_capsule = ctypes.pythonapi.PyCapsule_New
     new_capsule.restype = ctypes.py_object
     new_capsule.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
-    return torch.utils.dlpack.from_dlpack(new_capsule(managed, _DLTENSOR, None))
+    try:
+        return torch.utils.dlpack.from_dlpack(new_capsule(managed, _DLTENSOR, None))
+    except Exception:
+        lib.rtpb_buffer_free(handle)       # not imported: the buffer goes back to the pool
+        raise
 
 
 def trim_history_buffers():

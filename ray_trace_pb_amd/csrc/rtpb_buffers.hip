@@ -130,7 +130,8 @@ void managed_deleter(DLManagedTensor* t) {
 
 extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void** ptr,
                                  void** handle) {
-    if (!ptr || !handle || bytes == 0) return fail(RTPB_E_INVALID, "rtpb_buffer_alloc: null output or zero size");
+    if (!ptr || !handle || bytes == 0 || bytes > (1ull << 50))
+        return fail(RTPB_E_INVALID, "rtpb_buffer_alloc: null output, zero size or more than 1 PiB");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
