@@ -123,10 +123,12 @@ int rtpb_shutdown(void);
    plain fill of the same memory does not.  rtpb_buffer_alloc maps the buffer's physical
    memory in `chunk_bytes` chunks (0: 64 MiB) placed in the virtual range in a shuffled order (`seed`), so
    every buffer gets the fast rate.  The buffer is device memory like any other (pass `*ptr` to rtpb_trace).
-   rtpb_buffer_free synchronises the device (no kernel may still use the buffer) and keeps the buffer,
-   still mapped, in a pool: the next rtpb_buffer_alloc of the same size on that device returns it again
-   (a virtual range is never unmapped and mapped anew).  rtpb_buffer_trim -- and rtpb_shutdown, and an
-   allocation that finds the device full -- releases the physical memory of every pooled buffer.
+   rtpb_buffer_free keeps the buffer, still mapped, in a pool: the next rtpb_buffer_alloc of the same size
+   on that device returns it again -- stream-ordered reuse, like PyTorch's caching allocator (a virtual
+   range is never unmapped and mapped anew).  Besides the most recently freed buffer the pool holds at most
+   a quarter of a device's memory;
+   rtpb_buffer_trim -- and rtpb_shutdown, and an allocation that finds the device full -- synchronises the
+   device and releases the physical memory of every pooled buffer.
    rtpb_buffer_dlpack wraps the whole buffer as a C-contiguous DLPack (v0.8 DLManagedTensor, device type
    ROCm) tensor of `ndim` extents `shape` and element type `dtype` (RTPB_F64 / RTPB_F32); ownership passes
    to the importer, whose call of the managed tensor's deleter frees the buffer.  Replaces nothing in the

@@ -11,11 +11,13 @@
 //
 // Lifetime: the caller frees a buffer with rtpb_buffer_free, or hands it to a DLPack importer
 // (rtpb_buffer_dlpack) whose deleter frees it.  A freed buffer is kept, still mapped, in a per-process pool
-// and handed out again to the next allocation of the same size on the same device (after the device was
-// synchronised, so no kernel still uses it); a virtual range is never unmapped and then mapped again.
-// rtpb_buffer_trim (and rtpb_shutdown) releases the physical memory of every pooled buffer; its virtual range
-// stays reserved and unused, so no translation cached by the GPU can ever point a new buffer at released
-// memory.
+// and handed out again to the next allocation of the same size on the same device -- stream-ordered reuse,
+// as PyTorch's caching allocator does it (work queued on the same stream runs after the work that used the
+// buffer before); a virtual range is never unmapped and then mapped again.  Besides the most recently freed
+// buffer the pool holds at most a quarter of the device's memory; beyond that, and on rtpb_buffer_trim /
+// rtpb_shutdown / an allocation that finds the device full, pooled buffers are released (after a device synchronisation: no kernel may still
+// use memory being unmapped).  A released buffer's virtual range stays reserved and unused, so no
+// translation cached by the GPU can ever point a new buffer at released memory.
 #include "rtpb_internal.h"
 
 #include <algorithm>
@@ -50,16 +52,37 @@ int destroy(Buffer* b) {
 std::mutex g_pool_mu;
 std::vector<Buffer*> g_pool;                       // freed buffers, still mapped, ready for reuse
 
-// Back to the pool once the device has finished every kernel that may use it.
+// Back to the pool (newest last); the oldest pooled buffers are released while the pool holds more than a
+// quarter of the device's memory.
 int release(Buffer* b) {
+    size_t total = 0;
     {
         DeviceGuard g(b->dev);
-        if (hipDeviceSynchronize() != hipSuccess)
-            return fail(RTPB_E_HIP, "rtpb_buffer_free: hipDeviceSynchronize failed");
+        size_t free_b = 0;
+        if (hipMemGetInfo(&free_b, &total) != hipSuccess) total = 0;
     }
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back(b);
-    return RTPB_OK;
+    std::vector<Buffer*> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool.push_back(b);
+        uint64_t held = 0;
+        for (Buffer* p : g_pool)
+            if (p->dev == b->dev) held += p->size;
+        for (size_t k = 0; k < g_pool.size() && held > total / 4;) {
+            Buffer* p = g_pool[k];
+            if (p->dev == b->dev && p != b) {
+                held -= p->size;
+                drop.push_back(p);
+                g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(k));
+            } else {
+                ++k;
+            }
+        }
+    }
+    int rc = RTPB_OK;
+    for (Buffer* p : drop)
+        if (destroy(p) != RTPB_OK) rc = RTPB_E_HIP;
+    return rc;
 }
 
 Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk) {

@@ -425,6 +425,23 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     return E.trace_host(low, last, sel, devs)
 
 
+# histories at least this large are allocated as pooled history buffers (placement): the
+# many-plane writes keep their fast rate whatever the physical state of the card
+POOLED_HISTORY_BYTES = 1 << 30
+
+
+def _default_history(code, last, sel, layout_code):
+    """The result buffer of a trace without out=: a pooled history_buffer for large histories, else None
+    (trace_device then allocates with torch)."""
+    import torch
+    n = last.shape[0]
+    elem = 8 if code == C.RTPB_F64 else 4
+    if len(sel) * n * 8 * elem < POOLED_HISTORY_BYTES:
+        return None
+    shape = (len(sel), n, 8) if layout_code == C.RTPB_AOS else (len(sel), 8, n)
+    return E.history_buffer(shape, torch.float64 if elem == 8 else torch.float32, last.device)
+
+
 def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out=None):
     """The torch-CUDA trace of trace_surfaces.  Tabulated materials (user n() overrides, Ebaf11) are
     lowered with the key set of the previous bundle traced through them when there is one, and the kernel
@@ -442,7 +459,8 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layou
         if full and k > 1:
             new = E.trace_device(low, last, sel[1:], miss=miss)
             return torch.cat((rays.to(new.dtype), new), dim=0)
-        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=out)
+        dst = out if out is not None else _default_history(code, last, sel, layout_code)
+        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=dst)
 
     tab = E.tabulated(materials)
     if not tab:

@@ -96,3 +96,31 @@ def test_buffer_abi_errors():
     m = ctypes.c_void_p()
     assert lib.rtpb_buffer_dlpack(h, 2, shape, C.RTPB_F64, ctypes.byref(m)) == C.RTPB_E_INVALID   # too large
     assert lib.rtpb_buffer_free(h) == 0
+
+
+def test_large_default_histories_are_pooled_buffers():
+    """System.ray_trace without out= allocates histories >= POOLED_HISTORY_BYTES as pooled history buffers:
+    the same buffer comes back once the previous result is dropped, and the history is bit-identical to a
+    trace into a torch.empty history."""
+    system, m0, m1, rays, ref = golden("c3_relay")
+    fan = torch.empty((4 * 1000 * 1000, 8), dtype=torch.float64, device=DEV)
+    rt.fan_into(fan, np.array([8.0, 0, 0]), np.pi / 180, 2000, 0.635, 2000)
+    planes = 2 * len(system.surfaces) + 1
+    assert planes * fan.shape[0] * 8 * 4 >= rt.POOLED_HISTORY_BYTES
+    h1 = system.ray_trace(fan, m0, m1, dtype="float32")
+    p1 = h1.data_ptr()
+    ref_t = torch.empty_like(h1)
+    system.ray_trace(fan, m0, m1, dtype="float32", out=ref_t)
+    assert torch.equal(torch.isnan(h1), torch.isnan(ref_t))
+    assert bool(((h1 == ref_t) | torch.isnan(ref_t)).all())
+    assert torch.equal(h1.view(torch.int32), ref_t.view(torch.int32))
+    del h1
+    gc.collect()
+    h2 = system.ray_trace(fan, m0, m1, dtype="float32")
+    assert h2.data_ptr() == p1
+    assert torch.equal(h2.view(torch.int32), ref_t.view(torch.int32))
+    small = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)        # small: torch's allocator
+    assert same_bits(small.cpu().numpy(), ref)
+    del h2
+    gc.collect()
+    C.check(C.lib().rtpb_buffer_trim())
