@@ -27,6 +27,9 @@ sample of C3, plus C1 (BASELINE configs[0], the plano-convex CPU case).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--configs c2,c4,c5 | none]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1) outside torchrun starts `torch.distributed.run --nproc-per-node N` on
+itself as a child process and exits with its code; the ranks' JSON line (rank 0) is forwarded as is.
 """
 import argparse
 import json
@@ -82,12 +85,71 @@ def parse():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
                     help="measure HBM bytes / FLOPs with separate rocprofv3 --pmc child runs (rank 0, N=1)")
+    ap.add_argument("--extras", default="on", choices=["on", "off"],
+                    help="off: only the headline loop's launches (no placement check / drop-in calls), e.g. "
+                         "under rocprofv3 so the kernel's csv average is the timed launches'")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow --gpus N above the visible GPU count (ranks share GPUs: a rehearsal, not a measurement)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_argv(gpus, argv, port):
+    """The torchrun command that runs this script as `gpus` ranks (one process per GPU) with the same
+    arguments: `python bench.py --gpus N` launched without torchrun starts it as a child process."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(args, world, visible):
+    """--gpus N must name the job's world size; N GPUs must be visible unless --oversubscribe (rehearsal)."""
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU with "
+                         f"--gpus equal to the number of ranks")
+    if args.gpus > visible and not args.oversubscribe:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible (use --oversubscribe "
+                         f"to rehearse several ranks on shared GPUs)")
+
+
+def launch_ranks(args):
+    """No torchrun environment and N > 1: run `torchrun --nproc-per-node N bench.py <same args>` as a child
+    process (never exec: the parent has not touched the GPU, but nothing is replaced either), forward its
+    output and return its exit code."""
+    import torch
+    visible = torch.cuda.device_count()          # counts devices without initialising the GPU on this image
+    check_world(args, args.gpus, visible)
+    cmd = launcher_argv(args.gpus, sys.argv[1:], _free_port())
+    _log(f"launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, stdin=subprocess.DEVNULL).returncode
+
+
+def device_identity(dev):
+    """The rank's GPU: index, PCI domain:bus:device and UUID (distinct physical GPUs are checkable)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    return {"device": dev.index, "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                                       f"{getattr(p, 'pci_device_id', 0):02x}",
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name}
+
+
+def _gather_objects(world, obj):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 class Workload:
@@ -193,14 +255,14 @@ class Workload:
             self.out = main_out
         return kernel_ms
 
-    def e2e(self, reps=5):
+    def e2e(self, reps=15):
         """The drop-in call on device-resident rays: System.ray_trace(torch rays, m0, m1, dtype) -- lowering,
         table keys, output allocation and the launch (ms per call, synchronised)."""
         import torch
         dt = "float32" if self.code != self._E.C.RTPB_F64 else None
-        # System.ray_trace allocates its own history: from PyTorch's caching allocator, which hands a repeated
-        # call the block the previous history freed -- here the timed loop's buffer (kept cached, not
-        # returned to the driver), so the drop-in call's kernel writes the same memory as the loop's
+        # System.ray_trace allocates its own history: a history of >= 1 GiB is a history buffer, and the
+        # library's pool hands a repeated call the buffer the previous history freed -- first the timed loop's
+        # own buffer, then the same one call after call (stream-ordered reuse on the launch stream)
         del self.out
         h = self.system.ray_trace(self.rays, self.m0, self.m1, dtype=dt)
         del h
@@ -609,10 +671,14 @@ def pmc_child(args, dev):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.pmc_child:
+        sys.exit(launch_ranks(args))
     rank, world, local = dist_env()
     import torch
 
-    # one GPU per rank; the modulo only matters when rehearsing several ranks on one GPU
+    if not args.pmc_child:
+        check_world(args, world, torch.cuda.device_count())
+    # one GPU per rank; the modulo only matters when rehearsing several ranks on one GPU (--oversubscribe)
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     if args.pmc_child:
@@ -634,11 +700,13 @@ def main():
     kernel_ms, elapsed = wl.timed(args.steps)
     _barrier(world)
     fill = wl.fill_rate() if rank == 0 else None
-    alt_ms = wl.second_buffer(args.steps) if (world == 1 and args.config in ("c3", "c2")) else None
-    e2e_ms, e2e_kernel_ms = wl.e2e() if args.config == "c3" else (None, None)
+    extras = args.extras == "on"
+    alt_ms = wl.second_buffer(args.steps) if (extras and world == 1 and args.config in ("c3", "c2")) else None
+    e2e_ms, e2e_kernel_ms = wl.e2e() if (extras and args.config == "c3") else (None, None)
     g = _gather(world, [elapsed, kernel_ms])
-    per_rank = [{"rank": r, "kernel_ms": x[1], "alg_GBps": wl.alg_bytes / (x[1] * 1e-3) / 1e9, "wall_s": x[0]}
-                for r, x in enumerate(g)]
+    ids = _gather_objects(world, device_identity(dev))
+    per_rank = [{"rank": r, "kernel_ms": x[1], "alg_GBps": wl.alg_bytes / (x[1] * 1e-3) / 1e9, "wall_s": x[0],
+                 **ids[r]} for r, x in enumerate(g)]
     elapsed = max(p["wall_s"] for p in per_rank)
     kernel_ms_max = max(p["kernel_ms"] for p in per_rank)
     total_units = world * wl.n * wl.S * args.steps
@@ -676,13 +744,12 @@ def main():
             line["e2e_kernel_ms"] = e2e_kernel_ms
             line["e2e_overhead_ms"] = e2e_ms - e2e_kernel_ms
             line["e2e_note"] = ("System.ray_trace(torch rays, Vacuum(), Vacuum(), dtype='float32') on the device-"
-                                "resident C3 bundle: lowering, Ebaf11 table keys (the previous bundle's, checked "
-                                "by the kernel's table-miss flag), history allocation, launch, synchronise. "
-                                "e2e_kernel_ms: the same call's kernel (HIP events; its history is the cached "
-                                "block of the timed loop's buffer); e2e_overhead_ms: the host-side cost of the "
-                                "drop-in call. Interleaved with the loop's launches the call's kernel takes the "
-                                "loop's time (tools/e2e_kernel_diff.py), so e2e_over_loop_kernel also carries "
-                                "the run-to-run drift between the two measurements")
+                                "resident C3 bundle, the median of 15 calls: lowering (memoised by content), "
+                                "Ebaf11 table keys (the previous bundle's, checked by the kernel's table-miss "
+                                "flag), history allocation (a pooled history buffer: the timed loop's own, "
+                                "reused), launch, miss-flag read, synchronise. e2e_kernel_ms: the same call's "
+                                "kernel (HIP events); e2e_overhead_ms: the host-side cost of the drop-in call "
+                                "(tools/e2e_phases.py splits it by phase)")
         if alt_ms is not None:
             line["placement_check"] = {
                 "kernel_ms_history_buffer": kernel_ms, "kernel_ms_torch_empty": alt_ms,
@@ -690,8 +757,11 @@ def main():
                         "in shuffled order, the product's out= buffer for repeated traces); kernel_ms_torch_empty: "
                         "the same launches into a torch.empty history (the default allocation of System.ray_trace "
                         "without out=), whose many-plane write rate depends on where it lands (DESIGN.md 5)"}
-        if world > 1:
-            line["per_rank"] = per_rank
+        line["per_rank"] = per_rank
+        line["distinct_gpus"] = len({(p["pci"], p["uuid"]) for p in per_rank})
+        if line["distinct_gpus"] < world:
+            line["config"]["oversubscribed"] = (f"{world} ranks on {line['distinct_gpus']} GPU(s): a rehearsal of "
+                                                f"the N>1 path, not a scaling measurement")
     del head
 
     configs = [c for c in args.configs.split(",") if c and c != "none"]

@@ -39,10 +39,12 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 5   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+#define RTPB_ABI_VERSION 6   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
                                 3: input element type separate from the storage type (in_dtype)
                                 4: + rtpb_trace_checked (table-miss flag)
-                                5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers) */
+                                5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers)
+                                6: stream-ordered history buffers: rtpb_buffer_alloc takes the stream,
+                                   + rtpb_buffer_record_stream / _held / _dlpack_discard */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -116,28 +118,41 @@ int rtpb_device_count(void);
 /* Release every device resource the library holds (plans must be destroyed first). */
 int rtpb_shutdown(void);
 
-/* ---- history buffers (ABI 5) ------------------------------------------------------------------ */
+/* ---- history buffers (ABI 5, stream-ordered since ABI 6) ---------------------------------------- */
 /* Output buffers for large histories.  The 2S+1 planes of a history are written concurrently, and that
    write pattern runs 15-45 % slower into some physical placements -- physically contiguous memory in
    particular, which the first large allocations of a process on an unfragmented card often are -- while a
    plain fill of the same memory does not.  rtpb_buffer_alloc maps the buffer's physical
    memory in `chunk_bytes` chunks (0: 64 MiB) placed in the virtual range in a shuffled order (`seed`), so
    every buffer gets the fast rate.  The buffer is device memory like any other (pass `*ptr` to rtpb_trace).
-   rtpb_buffer_free keeps the buffer, still mapped, in a pool: the next rtpb_buffer_alloc of the same size
-   on that device returns it again -- stream-ordered reuse, like PyTorch's caching allocator (a virtual
-   range is never unmapped and mapped anew).  Besides the most recently freed buffer the pool holds at most
-   a quarter of a device's memory;
-   rtpb_buffer_trim -- and rtpb_shutdown, and an allocation that finds the device full -- synchronises the
-   device and releases the physical memory of every pooled buffer.
+   Streams -- PyTorch caching-allocator semantics, made explicit:
+     * a buffer is allocated for `stream` (a hipStream_t, NULL = the device's null stream);
+     * rtpb_buffer_record_stream(ptr, s) marks a use of the live buffer containing `ptr` on another stream
+       `s` (returns 1, not an error, when `ptr` is not inside a live history buffer);
+     * rtpb_buffer_free never blocks: it records an event on the allocation stream and on every recorded
+       stream and keeps the buffer, still mapped, in a per-device pool;
+     * the next rtpb_buffer_alloc of the same size on that device returns it and makes ITS stream wait for
+       those events on the device (hipStreamWaitEvent): nothing the new owner queues can touch the memory
+       before the previous owner's recorded uses have finished.
+   The pool keeps the most recently freed buffer per device (rtpb_set_tuning("buffer_pool_buffers", k)
+   keeps k, 0 none); an older one is unmapped and its physical memory released once its events have
+   completed (checked without blocking on later calls); its virtual range stays reserved, never reused.  rtpb_buffer_trim -- and
+   rtpb_shutdown, and an allocation that finds the device full -- waits for those events and releases
+   every pooled buffer.  rtpb_buffer_held reports the bytes and buffers the pool still holds on `device`
+   (-1: all devices).
    rtpb_buffer_dlpack wraps the whole buffer as a C-contiguous DLPack (v0.8 DLManagedTensor, device type
    ROCm) tensor of `ndim` extents `shape` and element type `dtype` (RTPB_F64 / RTPB_F32); ownership passes
-   to the importer, whose call of the managed tensor's deleter frees the buffer.  Replaces nothing in the
-   reference (NumPy allocates its histories itself, RT:1229-1232). */
-int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void** ptr,
+   to the importer, whose call of the managed tensor's deleter frees the buffer.  rtpb_buffer_dlpack_discard
+   runs that deleter for a managed tensor no importer consumed.  Replaces nothing in the reference (NumPy
+   allocates its histories itself, RT:1229-1232). */
+int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void* stream, void** ptr,
                       void** handle);
 int rtpb_buffer_free(void* handle);
+int rtpb_buffer_record_stream(const void* ptr, void* stream);
 int rtpb_buffer_trim(void);
+int rtpb_buffer_held(int32_t device, uint64_t* bytes, int32_t* buffers);
 int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed);
+int rtpb_buffer_dlpack_discard(void* managed);
 
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
 /* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,
@@ -313,7 +328,8 @@ int rtpb_distinct_keys(int32_t device, const void* col, int32_t dtype, int64_t n
    "indexed_materials": 1 (default) = plans created from now on whose TABLE materials all share one
    key set (and that have no POLY6 material) also tabulate every other material at those keys, so the
    kernel reads n from LDS instead of evaluating Sellmeier dispersion per surface (bit-identical: the
-   host evaluates the kernel's own material_n); 0 = evaluate per surface. */
+   host evaluates the kernel's own material_n); 0 = evaluate per surface.
+   "buffer_pool_buffers": freed history buffers kept mapped per device for reuse (default 1, 0..1024). */
 int rtpb_set_tuning(const char* key, int64_t value);
 
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */

@@ -302,3 +302,23 @@ def ray_fan(pt, theta_max, n_thetas, wavelengths, nphis=1, center_ray=(0, 0, 1))
         out[:, 3 + k] = c[k] * np.cos(tt) + ex[k] * np.cos(pp) * np.sin(tt) + ey[k] * np.sin(pp) * np.sin(tt)
     out[:, 7] = wavelengths
     return out
+
+
+def ray_fan_rows(pt, theta_max, n_thetas, wavelengths, nphis, row0, row1, center_ray=(0, 0, 1)):
+    """Rays [row0 * n_thetas, row1 * n_thetas) of ``ray_fan(pt, theta_max, n_thetas, wavelengths, nphis)``
+    (whole phi rows; RT:45-96): the same operations on the same operands per ray, so the rows are
+    bit-identical to the corresponding slice of the whole fan -- for tracing a large fan in pieces."""
+    c = np.array(center_ray)
+    thetas = np.linspace(-theta_max, theta_max, n_thetas)
+    phis = np.arange(row0, row1) * 2 * np.pi / nphis
+    tt, pp = np.meshgrid(thetas, phis)
+    tt, pp = tt.ravel(), pp.ravel()
+    ex = np.cross(np.array([0, 1, 0]), c)
+    ex = ex / np.linalg.norm(ex)
+    ey = np.cross(c, ex)
+    out = np.zeros((n_thetas * (row1 - row0), 8))
+    out[:, 0:3] = np.array(pt, dtype=float).squeeze()
+    for k in range(3):
+        out[:, 3 + k] = c[k] * np.cos(tt) + ex[k] * np.cos(pp) * np.sin(tt) + ey[k] * np.sin(pp) * np.sin(tt)
+    out[:, 7] = wavelengths
+    return out

@@ -11,7 +11,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 5
+RTPB_ABI_VERSION = 6
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
@@ -53,10 +53,13 @@ SIGNATURES = {
     "rtpb_last_error": (ctypes.c_char_p, []),
     "rtpb_device_count": (ctypes.c_int, []),
     "rtpb_shutdown": (ctypes.c_int, []),
-    "rtpb_buffer_alloc": (ctypes.c_int, [_i32, _u64, _u64, _u64, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "rtpb_buffer_alloc": (ctypes.c_int, [_i32, _u64, _u64, _u64, _P, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
     "rtpb_buffer_free": (ctypes.c_int, [_P]),
+    "rtpb_buffer_record_stream": (ctypes.c_int, [_P, _P]),
     "rtpb_buffer_trim": (ctypes.c_int, []),
+    "rtpb_buffer_held": (ctypes.c_int, [_i32, ctypes.POINTER(_u64), ctypes.POINTER(_i32)]),
     "rtpb_buffer_dlpack": (ctypes.c_int, [_P, _i32, ctypes.POINTER(_i64), _i32, ctypes.POINTER(_P)]),
+    "rtpb_buffer_dlpack_discard": (ctypes.c_int, [_P]),
     "rtpb_plan_create": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _i32,
                                         ctypes.POINTER(_P)]),
     "rtpb_plan_destroy": (ctypes.c_int, [_P]),

@@ -38,6 +38,7 @@ def _f3(v):
 
 _LOWERED = collections.OrderedDict()
 _LOWERED_MAX = 64
+_memo_lock = threading.Lock()            # guards _LOWERED and _KEYS (traces may run on several threads)
 
 
 def _vec_key(v):
@@ -64,6 +65,12 @@ def _lower_key(surfaces, materials, wl, dtype):
             if lowered is not None:
                 parts.append((lowered[0], tuple(float(c) for c in lowered[1])))
             else:
+                # a tabulated material's n() values are memoised only when n() is known to depend on the
+                # wavelength and the instance's attributes alone: the package's own (Ebaf11), or a user
+                # subclass that declares it with ``rtpb_pure_n = True``.  Any other user n() -- which may
+                # read class attributes, globals or other mutable state -- is evaluated on every trace.
+                if not _pure_n(m):
+                    return None
                 fp = table_fingerprint([m])
                 if fp is None:
                     return None
@@ -73,6 +80,10 @@ def _lower_key(surfaces, materials, wl, dtype):
         return tuple(parts)
     except (TypeError, ValueError, AttributeError):
         return None
+
+
+def _pure_n(m):
+    return type(m).n.__module__ == __package__ + ".materials" or getattr(type(m), "rtpb_pure_n", False) is True
 
 
 def lower(surfaces, materials, wavelengths, dtype):
@@ -87,15 +98,17 @@ def lower(surfaces, materials, wavelengths, dtype):
         wl = np.asarray(wavelengths(), dtype=np.float64)
     key = _lower_key(surfaces, materials, wl, dtype)
     if key is not None:
-        low = _LOWERED.get(key)
-        if low is not None:
-            _LOWERED.move_to_end(key)
-            return low
+        with _memo_lock:
+            low = _LOWERED.get(key)
+            if low is not None:
+                _LOWERED.move_to_end(key)
+                return low
     low = _lower(surfaces, materials, (lambda: wl), dtype)
     if key is not None:
-        _LOWERED[key] = low
-        while len(_LOWERED) > _LOWERED_MAX:
-            _LOWERED.popitem(last=False)
+        with _memo_lock:
+            _LOWERED[key] = low
+            while len(_LOWERED) > _LOWERED_MAX:
+                _LOWERED.popitem(last=False)
     return low
 
 
@@ -232,27 +245,33 @@ def tabulated(materials):
 
 
 def table_fingerprint(materials):
-    """Hashable identity of the tabulated materials' n() (class + attribute values), or None."""
+    """Hashable identity of the tabulated materials' n() (class + attribute values), or None.  A material
+    may supply ``_rtpb_table_key()`` (a cheap hashable of everything its n() reads; Ebaf11 does)."""
     try:
-        return tuple((type(m).__module__, type(m).__qualname__, id(type(m)), _fp(vars(m))) for m in materials)
+        return tuple((type(m).__module__, type(m).__qualname__, id(type(m)),
+                      m._rtpb_table_key() if hasattr(m, "_rtpb_table_key") else _fp(vars(m))) for m in materials)
     except (_NoFingerprint, TypeError):
         return None
 
 
 def previous_keys(fp):
-    keys = _KEYS.get(fp) if fp is not None else None
-    if keys is not None:
-        _KEYS.move_to_end(fp)
+    if fp is None:
+        return None
+    with _memo_lock:
+        keys = _KEYS.get(fp)
+        if keys is not None:
+            _KEYS.move_to_end(fp)
     return keys
 
 
 def remember_keys(fp, keys):
     if fp is None:
         return
-    _KEYS[fp] = keys
-    _KEYS.move_to_end(fp)
-    while len(_KEYS) > _KEYS_MAX:
-        _KEYS.popitem(last=False)
+    with _memo_lock:
+        _KEYS[fp] = keys
+        _KEYS.move_to_end(fp)
+        while len(_KEYS) > _KEYS_MAX:
+            _KEYS.popitem(last=False)
 
 
 def lower_material(m, wavelengths):
@@ -425,12 +444,26 @@ _DLTENSOR = b"dltensor"
 _buffer_seed = itertools.count(1)
 
 
-def history_buffer(shape, dtype, device, chunk_bytes=0):
+def _capsule_api():
+    api = ctypes.pythonapi
+    api.PyCapsule_New.restype = ctypes.py_object
+    api.PyCapsule_New.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    api.PyCapsule_IsValid.restype = ctypes.c_int
+    api.PyCapsule_IsValid.argtypes = [ctypes.py_object, ctypes.c_char_p]
+    return api
+
+
+def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
     """A C-contiguous torch CUDA tensor of ``shape`` and ``dtype`` (float32 / float64) on ``device`` whose
     memory comes from rtpb_buffer_alloc: physical chunks (64 MiB) mapped in a shuffled order, so a history
     traced into it writes at the fast rate whatever the physical state of the card (a history's many-plane
-    write pattern runs 15-45 % slower into physically contiguous placements).  Use it for the
-    ``out=`` of repeated traces; freeing it synchronises its device."""
+    write pattern runs 15-45 % slower into physically contiguous placements).
+
+    Stream semantics are those of torch's caching allocator: the buffer is allocated for ``stream`` (default:
+    the device's current stream); a use on another stream must be recorded with :func:`record_stream`
+    (torch's own ``Tensor.record_stream`` does nothing for this memory).  Freeing never blocks: the buffer
+    returns to the library's pool (the newest freed buffer per device is kept mapped), and the next buffer
+    of the same size makes its stream wait for every recorded use of the previous owner."""
     import torch
     if dtype not in (torch.float32, torch.float64):
         raise ValueError("history_buffer: dtype must be torch.float32 or torch.float64")
@@ -445,10 +478,18 @@ def history_buffer(shape, dtype, device, chunk_bytes=0):
         nbytes *= v
     if nbytes == 0:
         return torch.empty(shape, dtype=dtype, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(torch.device("cuda", idx))
+    raw_stream = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
     lib = C.lib()
     ptr, handle = ctypes.c_void_p(), ctypes.c_void_p()
-    C.check(lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, next(_buffer_seed), ctypes.byref(ptr),
-                                  ctypes.byref(handle)))
+    seed = next(_buffer_seed)
+    if lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, seed, raw_stream, ctypes.byref(ptr), ctypes.byref(handle)):
+        # the device may be full of blocks torch's caching allocator holds: release them and retry once
+        torch.cuda.synchronize(idx)
+        torch.cuda.empty_cache()
+        C.check(lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, seed, raw_stream, ctypes.byref(ptr),
+                                      ctypes.byref(handle)))
     managed = ctypes.c_void_p()
     ext = (ctypes.c_int64 * len(shape))(*shape)
     rc = lib.rtpb_buffer_dlpack(handle, len(shape), ext, C.RTPB_F64 if elem == 8 else C.RTPB_F32,
@@ -456,20 +497,57 @@ def history_buffer(shape, dtype, device, chunk_bytes=0):
     if rc != 0:
         lib.rtpb_buffer_free(handle)
         C.check(rc)
-    new_capsule = ctypes.pythonapi.PyCapsule_New
-    new_capsule.restype = ctypes.py_object
-    new_capsule.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    api = _capsule_api()
+    capsule = api.PyCapsule_New(managed, _DLTENSOR, None)
     try:
-        return torch.utils.dlpack.from_dlpack(new_capsule(managed, _DLTENSOR, None))
+        return torch.utils.dlpack.from_dlpack(capsule)
     except Exception:
-        lib.rtpb_buffer_free(handle)       # not imported: the buffer goes back to the pool
+        # DLPack protocol: an importer that consumed the capsule renamed it and owns the deleter; only an
+        # unconsumed capsule is discarded here (its deleter frees the buffer and the managed tensor)
+        if api.PyCapsule_IsValid(capsule, _DLTENSOR):
+            lib.rtpb_buffer_dlpack_discard(managed)
         raise
 
 
+def record_stream(tensor, stream):
+    """``tensor.record_stream(stream)`` for every kind of device memory: torch's caching-allocator record,
+    plus the library's record when the tensor lies in a history buffer (rtpb_buffer_record_stream) -- torch
+    ignores memory it did not allocate, so a history_buffer (and any default System.ray_trace history of
+    POOLED_HISTORY_BYTES or more) used on a side stream must be recorded this way before it is freed."""
+    tensor.record_stream(stream)
+    if tensor.numel() == 0:
+        return
+    raw = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    rc = C.lib().rtpb_buffer_record_stream(tensor.data_ptr(), raw)
+    if rc < 0:
+        C.check(rc)
+
+
+def history_buffers_held(device=-1):
+    """(bytes, buffers) the library's history-buffer pool holds on ``device`` (-1: every device): freed
+    buffers kept mapped for reuse, and retired ones whose last uses have not completed yet."""
+    nb, cnt = ctypes.c_uint64(), ctypes.c_int32()
+    C.check(C.lib().rtpb_buffer_held(int(device), ctypes.byref(nb), ctypes.byref(cnt)))
+    return int(nb.value), int(cnt.value)
+
+
 def trim_history_buffers():
-    """Release the device memory of every freed history_buffer (the library keeps freed ones mapped for
-    reuse by the next buffer of the same size; rtpb_buffer_trim)."""
+    """Release the device memory of every freed history_buffer (the library keeps the newest freed one per
+    device mapped for reuse; rtpb_buffer_trim waits for their last recorded uses)."""
     C.check(C.lib().rtpb_buffer_trim())
+
+
+def device_empty(shape, dtype, device):
+    """torch.empty on a CUDA device; on an out-of-memory error the history-buffer pool (memory torch cannot
+    see) is released and the allocation retried once."""
+    import torch
+    try:
+        return torch.empty(shape, dtype=dtype, device=device)
+    except torch.OutOfMemoryError:
+        if history_buffers_held()[1] == 0:
+            raise
+        trim_history_buffers()
+        return torch.empty(shape, dtype=dtype, device=device)
 
 
 def check_out(out, shape, dtype, device):
@@ -494,16 +572,22 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     n = rays.shape[0]
     if out is None:
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
-        out = torch.empty(shape, dtype=tdt, device=rays.device)
+        out = device_empty(shape, tdt, rays.device)
     lo, hi = plane_mask(planes)
     if stream is None:
         stream = torch.cuda.current_stream(rays.device).cuda_stream
+    lib = C.lib()
     with plan_ref(low) as plan:
         if miss is None:
-            C.check(C.lib().rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
-                                       out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+            C.check(lib.rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
+                                   out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
         else:
-            C.check(C.lib().rtpb_trace_checked(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
-                                               0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream,
-                                               miss.data_ptr()))
+            C.check(lib.rtpb_trace_checked(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
+                                           0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr()))
+    if n:
+        # a history buffer (out=, or rays read from a previous history) used on this stream: recorded, so a
+        # later owner of the memory waits for this launch (a no-op for the allocation stream and for memory
+        # that is not a history buffer)
+        lib.rtpb_buffer_record_stream(out.data_ptr(), stream)
+        lib.rtpb_buffer_record_stream(rays.data_ptr(), stream)
     return out

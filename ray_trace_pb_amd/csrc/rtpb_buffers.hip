@@ -1,4 +1,5 @@
-// rtpb_buffers.hip -- device buffers for large ray histories (rtpb_buffer_alloc / _free / _dlpack, ABI 5).
+// rtpb_buffers.hip -- device buffers for large ray histories (rtpb_buffer_alloc / _free / _dlpack /
+// _record_stream, ABI 6).
 //
 // A history is 2S+1 planes written concurrently by every wave (C3: 19 float32 planes of 1.6 GB).  That
 // many-plane write pattern runs at a rate that depends on where the buffer's physical memory lies: into a
@@ -9,18 +10,25 @@
 // shuffle (HIP virtual memory API), so the relative physical placement of the planes is randomised whatever
 // the state of VRAM: every such buffer measured at the fast rate.
 //
-// Lifetime: the caller frees a buffer with rtpb_buffer_free, or hands it to a DLPack importer
-// (rtpb_buffer_dlpack) whose deleter frees it.  A freed buffer is kept, still mapped, in a per-process pool
-// and handed out again to the next allocation of the same size on the same device -- stream-ordered reuse,
-// as PyTorch's caching allocator does it (work queued on the same stream runs after the work that used the
-// buffer before); a virtual range is never unmapped and then mapped again.  Besides the most recently freed
-// buffer the pool holds at most a quarter of the device's memory; beyond that, and on rtpb_buffer_trim /
-// rtpb_shutdown / an allocation that finds the device full, pooled buffers are released (after a device synchronisation: no kernel may still
-// use memory being unmapped).  A released buffer's virtual range stays reserved and unused, so no
-// translation cached by the GPU can ever point a new buffer at released memory.
+// Lifetime and streams (the semantics of PyTorch's caching allocator, made explicit):
+//   * a buffer is allocated FOR a stream (its allocation stream); work on that stream is ordered anyway;
+//   * rtpb_buffer_record_stream(ptr, s) marks a use on another stream s (torch's Tensor.record_stream, which
+//     does nothing for memory torch did not allocate -- io.HistoryWriter and ray_trace_pb_amd.record_stream
+//     call both);
+//   * freeing (rtpb_buffer_free, or the DLPack deleter) records one event on the allocation stream and on
+//     every recorded stream -- it never blocks;
+//   * a freed buffer stays mapped in a per-device pool; the next allocation of the same size on that device
+//     takes it and makes ITS stream wait (hipStreamWaitEvent, on the device) for those events, so no kernel
+//     of the new owner can touch the memory before the previous owner's last recorded use has finished;
+//   * the pool keeps only the most recently freed buffer per device (rtpb_set_tuning("buffer_pool_buffers")
+//     sets k, 0 = none); older ones retire: each is unmapped and its physical memory released (its virtual
+//     range kept reserved) once its events have completed -- checked without blocking on every
+//     later alloc / free, and waited for by rtpb_buffer_trim, rtpb_shutdown and an allocation that finds the
+//     device full.
 #include "rtpb_internal.h"
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -34,79 +42,174 @@ struct Buffer {
     size_t size = 0, chunk = 0;
     std::vector<hipMemGenericAllocationHandle_t> chunks;   // created physical chunks
     std::vector<uint64_t> mapped;                          // virtual slot of each mapped chunk
+    hipStream_t alloc_stream = nullptr;                    // the stream the current owner allocated it for
+    std::vector<hipStream_t> used;                         // other streams recorded by the current owner
+    std::vector<hipEvent_t> pending;                       // after free: the owner's last use on each stream
 };
 
-// Unmaps and releases the physical chunks of a buffer no one uses; its virtual range stays reserved (never
-// reused), the Buffer object is deleted.
+std::mutex g_mu;                                 // guards everything below
+std::map<uintptr_t, Buffer*> g_live;             // buffers owned by a caller, by virtual address
+std::vector<Buffer*> g_pool;                     // freed, still mapped, ready for reuse (newest last)
+std::vector<Buffer*> g_retired;                  // freed, leaving the pool: destroyed once `pending` is done
+size_t g_pool_keep = 1;                          // pooled buffers kept per device
+
+int stream_device(hipStream_t s, int fallback) {
+    int d = fallback;
+    if (s != nullptr && hipStreamGetDevice(s, &d) != hipSuccess) d = fallback;
+    return d;
+}
+
+bool events_done(const Buffer* b) {
+    for (hipEvent_t e : b->pending)
+        if (hipEventQuery(e) != hipSuccess) return false;
+    return true;
+}
+
+void drop_events(Buffer* b) {
+    for (hipEvent_t e : b->pending) (void)hipEventDestroy(e);
+    b->pending.clear();
+}
+
+// Unmaps and releases the physical chunks of a buffer, after waiting for the recorded uses of its last owner
+// (b->pending); its virtual range stays reserved and unused.  The Buffer object is deleted.
 int destroy(Buffer* b) {
     DeviceGuard g(b->dev);
-    hipError_t e = hipDeviceSynchronize();
+    hipError_t e = hipSuccess;
+    for (hipEvent_t ev : b->pending)
+        if (hipEventSynchronize(ev) != hipSuccess) e = hipErrorUnknown;
+    drop_events(b);
     for (uint64_t s : b->mapped)
         if (hipMemUnmap(static_cast<char*>(b->va) + s * b->chunk, b->chunk) != hipSuccess) e = hipErrorUnknown;
     for (auto h : b->chunks)
         if (hipMemRelease(h) != hipSuccess) e = hipErrorUnknown;
+    // The virtual range is NOT freed: a range freed and reserved again by a later buffer was seen to take
+    // writes through translations still cached for the old mapping (partial histories, profiles/r04/
+    // buffers_va_reuse.log).  Kept reserved it is never touched again; the cost is address space only.
     delete b;
     return e == hipSuccess ? RTPB_OK : fail(RTPB_E_HIP, "rtpb_buffer: releasing a mapping failed");
 }
 
-std::mutex g_pool_mu;
-std::vector<Buffer*> g_pool;                       // freed buffers, still mapped, ready for reuse
-
-// Back to the pool (newest last); the oldest pooled buffers are released while the pool holds more than a
-// quarter of the device's memory.
-int release(Buffer* b) {
-    size_t total = 0;
-    {
-        DeviceGuard g(b->dev);
-        size_t free_b = 0;
-        if (hipMemGetInfo(&free_b, &total) != hipSuccess) total = 0;
+// Retired buffers whose last uses have completed (never blocks); caller holds g_mu.
+std::vector<Buffer*> collect_retired_locked() {
+    std::vector<Buffer*> done;
+    for (size_t k = 0; k < g_retired.size();) {
+        if (events_done(g_retired[k])) {
+            done.push_back(g_retired[k]);
+            g_retired.erase(g_retired.begin() + static_cast<std::ptrdiff_t>(k));
+        } else {
+            ++k;
+        }
     }
-    std::vector<Buffer*> drop;
+    return done;
+}
+
+int destroy_all(const std::vector<Buffer*>& v) {
+    int rc = RTPB_OK;
+    for (Buffer* b : v)
+        if (destroy(b) != RTPB_OK) rc = RTPB_E_HIP;
+    return rc;
+}
+
+// The owner's last use on each stream it used, as events (the free itself never waits).
+int record_pending(Buffer* b) {
+    std::vector<hipStream_t> streams{b->alloc_stream};
+    for (hipStream_t s : b->used) streams.push_back(s);
+    b->used.clear();
+    int rc = RTPB_OK;
+    for (hipStream_t s : streams) {
+        DeviceGuard g(stream_device(s, b->dev));
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            rc = fail(RTPB_E_HIP, "rtpb_buffer_free: hipEventCreate failed");
+            (void)hipDeviceSynchronize();       // no event: the conservative fallback
+            continue;
+        }
+        if (hipEventRecord(ev, s) != hipSuccess) {
+            (void)hipEventDestroy(ev);
+            rc = fail(RTPB_E_HIP, "rtpb_buffer_free: hipEventRecord failed");
+            (void)hipDeviceSynchronize();
+            continue;
+        }
+        b->pending.push_back(ev);
+    }
+    return rc;
+}
+
+// Back to the pool (newest last); beyond g_pool_keep per device the oldest pooled buffers retire.
+int release(Buffer* b) {
+    int rc = record_pending(b);
+    std::vector<Buffer*> done;
     {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_live.erase(reinterpret_cast<uintptr_t>(b->va));
         g_pool.push_back(b);
-        uint64_t held = 0;
-        for (Buffer* p : g_pool)
-            if (p->dev == b->dev) held += p->size;
-        for (size_t k = 0; k < g_pool.size() && held > total / 4;) {
+        size_t held = 0;
+        for (Buffer* p : g_pool) held += p->dev == b->dev;
+        for (size_t k = 0; k < g_pool.size() && held > g_pool_keep;) {
             Buffer* p = g_pool[k];
-            if (p->dev == b->dev && p != b) {
-                held -= p->size;
-                drop.push_back(p);
+            if (p->dev == b->dev && (p != b || g_pool_keep == 0)) {
+                --held;
+                g_retired.push_back(p);
                 g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(k));
             } else {
                 ++k;
             }
         }
+        done = collect_retired_locked();
     }
-    int rc = RTPB_OK;
-    for (Buffer* p : drop)
-        if (destroy(p) != RTPB_OK) rc = RTPB_E_HIP;
+    if (destroy_all(done) != RTPB_OK) rc = RTPB_E_HIP;
     return rc;
 }
 
-Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (size_t k = 0; k < g_pool.size(); ++k) {
-        Buffer* b = g_pool[k];
-        if (b->dev == dev && b->size == size && b->chunk == chunk) {
-            g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(k));
-            return b;
+// A pooled buffer of this size for `stream`: the stream waits (on the device) for the previous owner's uses.
+Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk, hipStream_t stream) {
+    Buffer* b = nullptr;
+    std::vector<Buffer*> done;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (size_t k = g_pool.size(); k-- > 0;) {
+            Buffer* p = g_pool[k];
+            if (p->dev == dev && p->size == size && p->chunk == chunk) {
+                g_pool.erase(g_pool.begin() + static_cast<std::ptrdiff_t>(k));
+                b = p;
+                break;
+            }
         }
+        done = collect_retired_locked();
     }
-    return nullptr;
+    (void)destroy_all(done);
+    if (!b) return nullptr;
+    for (hipEvent_t ev : b->pending) {
+        if (hipEventQuery(ev) == hipSuccess) continue;
+        if (hipStreamWaitEvent(stream, ev, 0) != hipSuccess) (void)hipEventSynchronize(ev);
+    }
+    drop_events(b);
+    return b;
 }
 
-int trim_pool() {
+// Every pooled and retired buffer of `dev` (-1: all devices), waiting for their last uses.
+int trim_pool(int dev) {
     std::vector<Buffer*> all;
     {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        all.swap(g_pool);
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (auto* list : {&g_pool, &g_retired})
+            for (size_t k = 0; k < list->size();) {
+                if (dev < 0 || (*list)[k]->dev == dev) {
+                    all.push_back((*list)[k]);
+                    list->erase(list->begin() + static_cast<std::ptrdiff_t>(k));
+                } else {
+                    ++k;
+                }
+            }
     }
-    int rc = RTPB_OK;
-    for (Buffer* b : all)
-        if (destroy(b) != RTPB_OK) rc = RTPB_E_HIP;
-    return rc;
+    return destroy_all(all);
+}
+
+void own(Buffer* b, hipStream_t stream) {
+    b->alloc_stream = stream;
+    b->used.clear();
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_live[reinterpret_cast<uintptr_t>(b->va)] = b;
 }
 
 // splitmix64: the shuffle's generator
@@ -151,13 +254,26 @@ void managed_deleter(DLManagedTensor* t) {
 
 }  // namespace
 
-extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void** ptr,
-                                 void** handle) {
+namespace rtpbi {
+// rtpb_set_tuning("buffer_pool_buffers", k): pooled buffers kept per device (>= 0)
+int set_buffer_pool_keep(int64_t k) {
+    if (k < 0 || k > 1024) return fail(RTPB_E_INVALID, "rtpb_set_tuning: buffer_pool_buffers must be 0..1024");
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_pool_keep = static_cast<size_t>(k);
+    }
+    return RTPB_OK;
+}
+}  // namespace rtpbi
+
+extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void* stream,
+                                 void** ptr, void** handle) {
     if (!ptr || !handle || bytes == 0 || bytes > (1ull << 50))
         return fail(RTPB_E_INVALID, "rtpb_buffer_alloc: null output, zero size or more than 1 PiB");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
+    const auto st = static_cast<hipStream_t>(stream);
     DeviceGuard g(device);
     hipMemAllocationProp prop = {};
     prop.type = hipMemAllocationTypePinned;
@@ -171,7 +287,8 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     // a buffer smaller than one chunk is a single chunk of its own (rounded) size
     const uint64_t chunk = round_up(std::min<uint64_t>(want, round_up(bytes, gran)), gran);
     const uint64_t n = (bytes + chunk - 1) / chunk;
-    if (Buffer* p = take_pooled(device, n * chunk, chunk)) {
+    if (Buffer* p = take_pooled(device, n * chunk, chunk, st)) {
+        own(p, st);
         *ptr = p->va;
         *handle = p;
         return RTPB_OK;
@@ -194,14 +311,16 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     for (uint64_t k = n; k > 1; --k) std::swap(slot[k - 1], slot[mix(x) % k]);     // Fisher-Yates
     b->chunks.reserve(n);
     b->mapped.reserve(n);
+    bool trimmed = false;
     for (uint64_t k = 0; k < n; ++k) {
         hipMemGenericAllocationHandle_t h;
         if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
-            // out of memory: release the pooled buffers' memory once and retry
-            if (trim_pool() != RTPB_OK || hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+            // out of memory: release the pooled and retired buffers of this device once and retry
+            if (trimmed || trim_pool(device) != RTPB_OK || hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
                 (void)destroy(b);
                 return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemCreate failed (out of device memory?)");
             }
+            trimmed = true;
         }
         b->chunks.push_back(h);
         if (hipMemMap(static_cast<char*>(b->va) + slot[k] * chunk, chunk, 0, h, 0) != hipSuccess) {
@@ -217,6 +336,7 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
         (void)destroy(b);
         return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemSetAccess failed");
     }
+    own(b, st);
     *ptr = b->va;
     *handle = b;
     return RTPB_OK;
@@ -227,7 +347,41 @@ extern "C" int rtpb_buffer_free(void* handle) {
     return release(static_cast<Buffer*>(handle));
 }
 
-extern "C" int rtpb_buffer_trim(void) { return trim_pool(); }
+extern "C" int rtpb_buffer_record_stream(const void* ptr, void* stream) {
+    const auto p = reinterpret_cast<uintptr_t>(ptr);
+    const auto st = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_live.upper_bound(p);
+    if (it == g_live.begin()) return 1;
+    --it;
+    Buffer* b = it->second;
+    if (p >= it->first + b->size) return 1;                   // not inside a live history buffer
+    if (st != b->alloc_stream && std::find(b->used.begin(), b->used.end(), st) == b->used.end())
+        b->used.push_back(st);
+    return RTPB_OK;
+}
+
+extern "C" int rtpb_buffer_trim(void) { return trim_pool(-1); }
+
+extern "C" int rtpb_buffer_held(int32_t device, uint64_t* bytes, int32_t* buffers) {
+    if (!bytes || !buffers) return fail(RTPB_E_INVALID, "rtpb_buffer_held: null output");
+    uint64_t tot = 0;
+    int32_t cnt = 0;
+    std::vector<Buffer*> done;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        done = collect_retired_locked();
+        for (auto* list : {&g_pool, &g_retired})
+            for (Buffer* b : *list)
+                if (device < 0 || b->dev == device) {
+                    tot += b->size;
+                    ++cnt;
+                }
+    }
+    *bytes = tot;
+    *buffers = cnt;
+    return destroy_all(done);
+}
 
 extern "C" int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed) {
     if (!handle || !managed || ndim < 1 || ndim > 8 || !shape)
@@ -254,5 +408,12 @@ extern "C" int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* sha
     m->t.manager_ctx = m;
     m->t.deleter = managed_deleter;
     *managed = &m->t;
+    return RTPB_OK;
+}
+
+extern "C" int rtpb_buffer_dlpack_discard(void* managed) {
+    if (!managed) return fail(RTPB_E_INVALID, "rtpb_buffer_dlpack_discard: null");
+    auto* t = static_cast<DLManagedTensor*>(managed);
+    t->deleter(t);
     return RTPB_OK;
 }

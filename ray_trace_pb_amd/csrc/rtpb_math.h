@@ -114,12 +114,9 @@ struct GuardDefer { static constexpr bool kDefer = true; bool bad = false; };
 // (iii) and (iv) are identities (a negative or NaN x gives NaN either way), so the device path runs step
 // (ii) alone -- the identical instructions, hence identical bits -- and hands the remaining inputs
 // (+-0, denormals, tiny normals, +inf) to the full expansion.
-template <typename T, class G = GuardBranch>
-RTPB_HD T tsqrt(T v, G* g = nullptr) {
-    if constexpr (sizeof(T) != 8) {
-        return sqrtf(v);
-    } else {
 #if defined(RTPB_FASTSQRT)
+// step (ii) alone: RN(sqrt(v)) for 2^-767 <= v < inf, NaN for v < 0 and v NaN
+__device__ __forceinline__ double sqrt_core(double v) {
     const double y = __builtin_amdgcn_rsq(v);
     const double s0 = v * y;
     const double h0 = y * 0.5;
@@ -129,7 +126,17 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     const double h1 = __builtin_fma(h0, r0, h0);
     const double s2 = __builtin_fma(d0, h1, s1);
     const double d1 = __builtin_fma(-s2, s2, v);
-    double s3 = __builtin_fma(d1, h1, s2);
+    return __builtin_fma(d1, h1, s2);
+}
+#endif
+
+template <typename T, class G = GuardBranch>
+RTPB_HD T tsqrt(T v, G* g = nullptr) {
+    if constexpr (sizeof(T) != 8) {
+        return sqrtf(v);
+    } else {
+#if defined(RTPB_FASTSQRT)
+    double s3 = sqrt_core(v);
     // the set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
     // compare of the high word (negative values and NaN have it at or above 0x10000000 unsigned)
     // (bitwise |: both tests are one VALU each; a short-circuit || puts the core under a branch of its own)
@@ -299,6 +306,27 @@ RTPB_HD Rcp<T> make_rcp(T b) {
 #endif
     return Rcp<T>{b, T(0), true, T(0)};
 }
+
+#if defined(RTPB_FASTDIV) && defined(RTPB_FASTSQRT)
+// Norms of 3-vectors, fused: for v = (x x + y y) + z z in [2^-240, 2^238), sqrt(v) takes the fast core
+// (v >= 2^-767, finite) and nrm = RN(sqrt(v)) lies in [2^-120, 2^119], inside the shared-divisor range of
+// fastdiv_den_ok -- so ONE test on v (its high word: the bounds have zero low words) replaces the square
+// root's class / high-word test and the divisor's frexp test.  NaN v also takes the fast path (the core,
+// the reciprocal and the quotients all give NaN, as the full sequences do).
+__device__ __forceinline__ bool norm2_fast(double v) {
+    const uint32_t hi = static_cast<uint32_t>(__double2hiint(v));
+    return (hi - 0x30F00000u < 0x4ED00000u - 0x30F00000u) | (v != v);
+}
+
+// make_rcp for a divisor known to be in range (or NaN): the same instructions without the test
+__device__ __forceinline__ Rcp<double> make_rcp_in_range(double b) {
+    const double y0 = __builtin_amdgcn_rcp(b);
+    const double y1 = __builtin_fma(y0, __builtin_fma(-b, y0, 1.0), y0);
+    const double y2 = __builtin_fma(y1, __builtin_fma(-b, y1, 1.0), y1);
+    return Rcp<double>{b, y2, true, 0.0};
+}
+#define RTPB_FASTNORM 1
+#endif
 
 // a / r.b
 template <typename T, class G = GuardBranch>
@@ -537,8 +565,23 @@ RTPB_HD bool positive_finite(T v) {
 }
 
 // v / |v| with NaN components replaced by 0 (RT:1203-1209)
-template <typename T, class G = GuardBranch>
+// FUSED (the trace kernels' own surface steps): a NaN norm -- a NaN or infinite component of d x N or N x b,
+// i.e. a NaN / infinite direction or normal -- leaves NaN quotients instead of zeros.  Every such ray is
+// killed by the surface's own on-surface test in the same step (its intersection is NaN or infinite: the
+// direction entered the intersection, and a sphere's normal is NaN only where its intersection is), so the
+// stored values are the same; the user-geometry kernels (rtpb_interact, normals from user code) keep the
+// exact fix-ups.  A finite in-range norm squared takes the combined test (norm2_fast) instead of three.
+template <bool FUSED = false, typename T, class G = GuardBranch>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
+#if defined(RTPB_FASTNORM)
+    if constexpr (FUSED && sizeof(T) == 8 && !G::kDefer) {
+        const T v = x * x + y * y + z * z;
+        if (__builtin_expect(norm2_fast(v), 1)) {
+            div3_norm(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
+            return;
+        }
+    }
+#endif
     const T nrm = tsqrt<T>(x * x + y * y + z * z, g);
     div3_norm(x, y, z, make_rcp(nrm), g);
     // A NaN quotient needs a zero, infinite or NaN norm: when 0 < |v| < inf every component is finite and
@@ -553,7 +596,7 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
 // AX: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot)
-template <bool AX = false, typename T, class G = GuardBranch>
+template <bool AX = false, bool FUSED = false, typename T, class G = GuardBranch>
 RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
     T bx, by, bz;
     if constexpr (AX) {
@@ -565,7 +608,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         by = ri.dz * Nx - ri.dx * Nz;
         bz = ri.dx * Ny - ri.dy * Nx;
     }
-    unit_or_zero(bx, by, bz, g);
+    unit_or_zero<FUSED>(bx, by, bz, g);
     if constexpr (AX) {
         cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
         cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
@@ -575,7 +618,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         cy = Nz * bx - Nx * bz;
         cz = Nx * by - Ny * bx;
     }
-    unit_or_zero(cx, cy, cz, g);
+    unit_or_zero<FUSED>(cx, cy, cz, g);
 }
 
 // np.sign(v) * root for root >= +0 or NaN (RT:1217; 1 - m^2 is never -0): for v < 0 or v > 0 the product is
@@ -590,10 +633,10 @@ RTPB_HD T signed_root(T v, T root) {
 // Snell refraction of the intersected ray (RT:1197-1221)
 // ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
 // AX: N == (+0, +0, 1) (axdot)
-template <bool AX = false, typename T, class G = GuardBranch>
+template <bool AX = false, bool FUSED = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis<AX>(ri, Nx, Ny, Nz, cx, cy, cz, g);
+    tangent_basis<AX, FUSED>(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
     const T tang = signed_root(axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz), tsqrt<T>(T(1) - mag * mag, g));
     Ray<T> o;
@@ -616,10 +659,10 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr
 }
 
 // law of reflection (RT:1267-1289)
-template <typename T, class G = GuardBranch>
+template <bool FUSED = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
+    tangent_basis<false, FUSED>(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag_na = -(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
     const T mag_nc = cx * ri.dx + cy * ri.dy + cz * ri.dz;
     Ray<T> o;
@@ -692,12 +735,37 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         } else {
             spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
         }
-        const T spn = tsqrt<T>(spx * spx + spy * spy + spz * spz, g);
-        if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
+        // |s1_perp| and |r1| (RT:1704-1728): a norm squared in range takes the combined test (norm2_fast), the
+        // rest the full tests -- bit-identical either way, NaN included
+        const T spv = spx * spx + spy * spy + spz * spz;
         const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
-        const T r1n = tsqrt<T>(r1x * r1x + r1y * r1y + r1z * r1z, g);
+        const T r1v = r1x * r1x + r1y * r1y + r1z * r1z;
         T ux = r1x, uy = r1y, uz = r1z;
-        if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
+        T r1n;
+#if defined(RTPB_FASTNORM)
+        if constexpr (sizeof(T) == 8 && !G::kDefer) {
+            if (__builtin_expect(norm2_fast(spv), 1)) {
+                const T spn = sqrt_core(spv);
+                if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp_in_range(spn), g);
+            } else {
+                const T spn = tsqrt<T>(spv, g);
+                if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
+            }
+            if (__builtin_expect(norm2_fast(r1v), 1)) {
+                r1n = sqrt_core(r1v);
+                div3_norm(ux, uy, uz, make_rcp_in_range(r1n), g);     // r1n >= 2^-120 or NaN: != 0
+            } else {
+                r1n = tsqrt<T>(r1v, g);
+                if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
+            }
+        } else
+#endif
+        {
+            const T spn = tsqrt<T>(spv, g);
+            if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
+            r1n = tsqrt<T>(r1v, g);
+            if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
+        }
         const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
         Ray<T> o;
         const T h = n1 * f * sin_t1;
@@ -738,7 +806,14 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             Nx = axsub<AX>(ri.x, s.c[0]);                                  // (p - c) / R, RT:1476
             Ny = axsub<AX>(ri.y, s.c[1]);
             Nz = ri.z - s.c[2];
-            div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
+            if constexpr (AX) {
+                // kAxial spheres have a finite shell_hi: where the on-surface test passes (the only rays whose
+                // normal reaches a stored value) each |p - c| component is below sqrt(shell_hi) < 2^513, so the
+                // numerators need only the lower bound of the exact range (div3_norm's single min3 test)
+                div3_norm(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
+            } else {
+                div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
+            }
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
             ri = to_plane<AX, AX>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
@@ -746,7 +821,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
-            after = reflect(ri, Nx, Ny, Nz, g);
+            after = reflect<true>(ri, Nx, Ny, Nz, g);
             kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
@@ -759,7 +834,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             } else {
                 ratio = n1 / n2;
             }
-            after = snell<AX && KIND == FLAT>(ri, Nx, Ny, Nz, ratio, g);
+            after = snell<AX && KIND == FLAT, true>(ri, Nx, Ny, Nz, ratio, g);
             const bool ok = (KIND == SPHERE) ? on_sphere<AX>(ri, s) : on_flat<AX>(ri, s);
             kill_if(!ok, after);
         }

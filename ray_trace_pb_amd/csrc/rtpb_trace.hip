@@ -356,6 +356,7 @@ int rtpb_set_tuning(const char* key, int64_t value) {
         g_indexed_materials.store(value != 0);
         return RTPB_OK;
     }
+    if (std::strcmp(key, "buffer_pool_buffers") == 0) return set_buffer_pool_keep(value);
     return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);
 }
 

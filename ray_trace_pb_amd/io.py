@@ -18,6 +18,8 @@ import threading
 
 import numpy as np
 
+from . import _engine as E
+
 ARRAY_COLUMNS = ["x", "y", "z", "dx", "dy", "dz", "phase", "wavelength"]
 
 
@@ -62,10 +64,11 @@ class HistoryWriter:
             item = self._q.get()
             if item is None:
                 return
-            index, arr, event, buf = item
+            index, arr, event, buf, src = item
             try:
                 if event is not None:
                     event.synchronize()
+                del src             # the device history may be freed (and its memory reused) from here on
                 tmp = self._chunk_file(index) + ".tmp"
                 with open(tmp, "wb") as f:
                     f.write(memoryview(np.ascontiguousarray(arr)).cast("B"))
@@ -99,10 +102,14 @@ class HistoryWriter:
                 buf.copy_(history, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(stream)
-            history.record_stream(stream)
-            self._q.put((index, buf.numpy(), ev, buf))
+            # the copy reads `history` on the side stream: recorded for torch's allocator AND for the
+            # library's history buffers (large default histories; torch's record_stream ignores them), and
+            # the queue item holds the tensor until the copy has finished, so its memory is not handed to
+            # the next trace while the copy is in flight (the next trace takes another buffer meanwhile)
+            E.record_stream(history, stream)
+            self._q.put((index, buf.numpy(), ev, buf, history))
         else:
-            self._q.put((index, np.asarray(history, dtype=self.dtype).copy(), None, None))
+            self._q.put((index, np.asarray(history, dtype=self.dtype).copy(), None, None, None))
 
     def write_array(self, name, values):
         """A small companion array (e.g. the swept parameter), like ``z.array(name, values)``."""

@@ -122,6 +122,10 @@ class Ebaf11(Material):
         # on ~5 % of wavelengths (AVX-512 hosts), and bit-exactness needs the reference's own n().
         return None
 
+    def _rtpb_table_key(self):
+        # everything n() reads (the lowering memo and the previous-bundle key cache are keyed by it)
+        return tuple(float(p) for p in self.params)
+
 
 def _glass(name, doc):
     b, c = _SELLMEIER[name]

@@ -353,6 +353,25 @@ def history_buffer(shape, dtype, device):
     return E.history_buffer(shape, dtype, device)
 
 
+def record_stream(tensor, stream):
+    """Mark a use of ``tensor`` on ``stream`` before it is freed -- torch's ``Tensor.record_stream``, extended
+    to history buffers (a :func:`history_buffer`, and any default history of ``POOLED_HISTORY_BYTES`` or
+    more), whose memory torch's allocator does not own: the next owner of that memory then waits for the
+    work queued on ``stream``."""
+    E.record_stream(tensor, stream)
+
+
+def trim_history_buffers():
+    """Release the device memory the history-buffer pool keeps for reuse (call it with
+    ``torch.cuda.empty_cache()`` to return all cached memory to the device)."""
+    E.trim_history_buffers()
+
+
+def history_buffers_held(device=-1):
+    """(bytes, buffers) of freed history buffers the pool still holds on ``device`` (-1: all devices)."""
+    return E.history_buffers_held(device)
+
+
 def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devices=None, layout="aos", gather=True,
                    out=None):
     """Trace ``rays`` through ``surfaces`` with ``materials`` (len(surfaces)+1 entries) on the GPU.
@@ -425,8 +444,9 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     return E.trace_host(low, last, sel, devs)
 
 
-# histories at least this large are allocated as pooled history buffers (placement): the
-# many-plane writes keep their fast rate whatever the physical state of the card
+# histories at least this large are allocated as history buffers (placement): the many-plane
+# writes keep their fast rate whatever the physical state of the card.  Stream-ordered like torch's
+# allocator; a use on another stream is recorded with record_stream (io.HistoryWriter does it)
 POOLED_HISTORY_BYTES = 1 << 30
 
 
@@ -500,7 +520,7 @@ def _trace_scattered(surfaces, materials, rays, devs, *, planes, dtype, layout, 
     axis = 2 if layout == "soa" else 1
     shape = list(outs[0].shape)
     shape[axis] = n
-    out = torch.empty(shape, dtype=outs[0].dtype, device=rays.device)
+    out = E.device_empty(shape, outs[0].dtype, rays.device)
     for (a, b), o in zip(shard_bounds(n, len(devs)), outs):
         out.narrow(axis, a, b - a).copy_(o, non_blocking=True)
     return out

@@ -39,3 +39,42 @@ def test_roofline_object_fields():
     assert abs(r["frac_of_output_fill"] - r["achieved_physical"] / 6800.0) < 1e-12
     assert r["torch_copy_GBps"] == 4700.0
     assert "torch_copy_GBps" not in bench.roofline(wl, 6.2)
+
+
+def test_launcher_argv_runs_this_script_as_n_ranks():
+    """`python bench.py --gpus N` outside torchrun starts torch.distributed.run on itself as a child process."""
+    import os
+    import sys
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "2"]
+    cmd = bench.launcher_argv(8, argv, 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    script = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[script + 1:] == argv                     # the same arguments reach every rank
+
+
+def test_world_size_checks_fail_loudly():
+    import pytest
+    args = types.SimpleNamespace(gpus=4, oversubscribe=False)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.check_world(args, 2, 8)                    # --gpus 4 under a 2-rank torchrun
+    with pytest.raises(SystemExit, match="only 2 GPU"):
+        bench.check_world(args, 4, 2)                    # more ranks than visible GPUs
+    bench.check_world(args, 4, 8)
+    bench.check_world(types.SimpleNamespace(gpus=4, oversubscribe=True), 4, 1)   # rehearsal on a shared GPU
+
+
+def test_bench_gpus_n_without_gpus_fails_before_launching():
+    """No GPU visible (this container): `bench.py --gpus 2` refuses before starting any rank."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--steps", "1"], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
+    assert r.stdout.strip() == ""

@@ -1,6 +1,7 @@
-"""Placement-robust history buffers (rtpb_buffer_alloc / _free / _dlpack, ABI 5) and ``ray_trace(..., out=)``:
-the buffer is ordinary device memory to the kernels (bit-identical histories), a torch tensor to the caller,
-and released when the tensor dies."""
+"""Placement-robust history buffers (rtpb_buffer_alloc / _free / _dlpack, ABI 5; stream-ordered since ABI 6)
+and ``ray_trace(..., out=)``: the buffer is ordinary device memory to the kernels (bit-identical histories),
+a torch tensor to the caller, released when the tensor dies, and never handed to a new owner while work of
+the previous owner -- on its allocation stream or on a recorded stream -- can still touch it."""
 import ctypes
 import gc
 import os
@@ -88,14 +89,29 @@ def test_buffers_are_pooled_and_trimmed():
 def test_buffer_abi_errors():
     lib = C.lib()
     p, h = ctypes.c_void_p(), ctypes.c_void_p()
-    assert lib.rtpb_buffer_alloc(0, 0, 0, 1, ctypes.byref(p), ctypes.byref(h)) == C.RTPB_E_INVALID
-    assert lib.rtpb_buffer_alloc(10_000, 1 << 20, 0, 1, ctypes.byref(p), ctypes.byref(h)) == C.RTPB_E_NODEV
+    assert lib.rtpb_buffer_alloc(0, 0, 0, 1, None, ctypes.byref(p), ctypes.byref(h)) == C.RTPB_E_INVALID
+    assert lib.rtpb_buffer_alloc(10_000, 1 << 20, 0, 1, None, ctypes.byref(p), ctypes.byref(h)) == C.RTPB_E_NODEV
     assert lib.rtpb_buffer_free(None) == C.RTPB_E_INVALID
-    assert lib.rtpb_buffer_alloc(0, 5 << 20, 2 << 20, 7, ctypes.byref(p), ctypes.byref(h)) == 0
+    assert lib.rtpb_buffer_alloc(0, 5 << 20, 2 << 20, 7, None, ctypes.byref(p), ctypes.byref(h)) == 0
     shape = (ctypes.c_int64 * 2)(1 << 30, 8)
     m = ctypes.c_void_p()
     assert lib.rtpb_buffer_dlpack(h, 2, shape, C.RTPB_F64, ctypes.byref(m)) == C.RTPB_E_INVALID   # too large
+    # record_stream: inside the live buffer -> recorded (0); outside any live buffer -> 1 (not an error)
+    s = torch.cuda.Stream(DEV)
+    assert lib.rtpb_buffer_record_stream(ctypes.c_void_p(p.value + 4096), s.cuda_stream) == 0
+    assert lib.rtpb_buffer_record_stream(ctypes.c_void_p(p.value + (6 << 20) + 64), s.cuda_stream) == 1
     assert lib.rtpb_buffer_free(h) == 0
+    assert lib.rtpb_buffer_record_stream(p, s.cuda_stream) == 1           # freed: no longer live
+    # a managed tensor no importer consumed is discarded through its own deleter (the buffer is pooled)
+    C.check(lib.rtpb_buffer_trim())
+    assert lib.rtpb_buffer_alloc(0, 5 << 20, 2 << 20, 7, None, ctypes.byref(p), ctypes.byref(h)) == 0
+    shape = (ctypes.c_int64 * 2)(1024, 8)
+    assert lib.rtpb_buffer_dlpack(h, 2, shape, C.RTPB_F64, ctypes.byref(m)) == 0
+    assert rt.history_buffers_held(0) == (0, 0)
+    assert lib.rtpb_buffer_dlpack_discard(m) == 0
+    assert rt.history_buffers_held(0)[1] == 1
+    C.check(lib.rtpb_buffer_trim())
+    assert rt.history_buffers_held() == (0, 0)
 
 
 def test_large_default_histories_are_pooled_buffers():
@@ -123,4 +139,179 @@ def test_large_default_histories_are_pooled_buffers():
     assert same_bits(small.cpu().numpy(), ref)
     del h2
     gc.collect()
+    C.check(C.lib().rtpb_buffer_trim())
+
+
+def _sleep_available():
+    return hasattr(torch.cuda, "_sleep")
+
+
+def _delay(stream, cycles=200_000_000):
+    """A kernel that spins on `stream` (torch.cuda._sleep) so that work queued after it on that stream runs
+    well after the host has moved on."""
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(cycles)
+
+
+@pytest.mark.skipif(not _sleep_available(), reason="torch.cuda._sleep is not available")
+def test_reuse_waits_for_the_previous_owners_allocation_stream():
+    """Freed on stream A while a (delayed) kernel on A still writes it; the next buffer of that size, taken
+    for stream B, is the same memory, and B's work runs only after A's: B's values survive."""
+    C.check(C.lib().rtpb_buffer_trim())
+    a, b = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    shape = (3, 1 << 20, 8)
+    from ray_trace_pb_amd import _engine as E
+    t = E.history_buffer(shape, torch.float32, DEV, stream=a)
+    p = t.data_ptr()
+    _delay(a)
+    with torch.cuda.stream(a):
+        t.fill_(1.0)                       # queued behind the spin: still pending when t is freed
+    del t
+    gc.collect()
+    u = E.history_buffer(shape, torch.float32, DEV, stream=b)
+    assert u.data_ptr() == p               # the pooled buffer
+    with torch.cuda.stream(b):
+        u.fill_(2.0)                       # must run after A's fill
+    torch.cuda.synchronize()
+    assert bool((u == 2.0).all())
+    del u
+    gc.collect()
+    C.check(C.lib().rtpb_buffer_trim())
+
+
+@pytest.mark.skipif(not _sleep_available(), reason="torch.cuda._sleep is not available")
+def test_reuse_waits_for_recorded_streams():
+    """Allocated for stream A, used on a side stream S (recorded with record_stream -- torch's own
+    Tensor.record_stream ignores this memory) and freed while S's work is pending; the next owner on A
+    waits for S."""
+    C.check(C.lib().rtpb_buffer_trim())
+    a, side = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    from ray_trace_pb_amd import _engine as E
+    shape = (5, 1 << 20, 8)
+    t = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    p = t.data_ptr()
+    _delay(side)
+    with torch.cuda.stream(side):
+        t.fill_(3.0)
+    rt.record_stream(t, side)
+    del t
+    gc.collect()
+    u = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    assert u.data_ptr() == p
+    with torch.cuda.stream(a):
+        u.fill_(4.0)
+    torch.cuda.synchronize()
+    assert bool((u == 4.0).all())
+    del u
+    gc.collect()
+    C.check(C.lib().rtpb_buffer_trim())
+
+
+def test_trace_on_a_side_stream_is_recorded():
+    """trace_device records its launch stream on an out= history buffer allocated for another stream: the
+    next owner of that memory waits for the trace."""
+    system, m0, m1, rays, ref = golden("c1_plano_convex")
+    from ray_trace_pb_amd import _engine as E
+    C.check(C.lib().rtpb_buffer_trim())
+    x = torch.from_numpy(np.tile(rays, (2000, 1))).to(DEV)
+    a, side = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    shape = (2 * len(system.surfaces) + 1, x.shape[0], 8)
+    out = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    p = out.data_ptr()
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        if _sleep_available():
+            torch.cuda._sleep(100_000_000)
+        system.ray_trace(x, m0, m1, out=out)
+    del out
+    gc.collect()
+    u = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    assert u.data_ptr() == p
+    with torch.cuda.stream(a):
+        u.fill_(-1.0)
+    torch.cuda.synchronize()
+    assert bool((u == -1.0).all())
+    del u
+    gc.collect()
+    C.check(C.lib().rtpb_buffer_trim())
+
+
+def test_pool_keeps_only_the_newest_buffer():
+    """After the results die, the pool holds one freed buffer per device (the newest), not every size seen:
+    memory torch cannot see stays bounded."""
+    C.check(C.lib().rtpb_buffer_trim())
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info()[0]
+    bufs = [rt.history_buffer((k, 1 << 27, 8), torch.float32, DEV) for k in (2, 3, 4)]     # 8, 12, 16 GiB
+    for t in bufs:
+        t[-1, -1].fill_(0.0)
+    del bufs, t
+    gc.collect()
+    torch.cuda.synchronize()
+    nbytes, nbuf = rt.history_buffers_held(0)
+    assert nbuf == 1 and nbytes == 4 << 32                       # the last one freed: 16 GiB
+    assert torch.cuda.mem_get_info()[0] >= free0 - (16 << 30) - (512 << 20)
+    C.check(C.lib().rtpb_buffer_trim())
+    assert torch.cuda.mem_get_info()[0] >= free0 - (512 << 20)
+
+
+def test_torch_allocation_takes_the_pooled_memory():
+    """A history allocation by torch that only fits in the memory the pool holds succeeds: on torch's
+    out-of-memory error the drop-in path releases the pool and retries (E.device_empty) -- here the
+    drop-in call itself, with a history below POOLED_HISTORY_BYTES (a torch allocation)."""
+    system, m0, m1, rays, ref = golden("c3_relay")
+    from ray_trace_pb_amd import _engine as E
+    C.check(C.lib().rtpb_buffer_trim())
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    big = rt.history_buffer((1, 5 << 30), torch.float64, DEV)         # 40 GiB, then freed into the pool
+    big[0, -1].fill_(0.0)
+    del big
+    gc.collect()
+    torch.cuda.synchronize()
+    assert rt.history_buffers_held(0)[1] == 1
+    fan = torch.empty((1000 * 1000, 8), dtype=torch.float64, device=DEV)
+    rt.fan_into(fan, np.array([8.0, 0, 0]), np.pi / 180, 1000, 0.635, 1000)
+    want = system.ray_trace(fan, m0, m1, dtype="float32").cpu()        # 0.6 GB history
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()                                           # its block must not be cached
+    free = torch.cuda.mem_get_info()[0]
+    filler = torch.empty(free - (256 << 20), dtype=torch.uint8, device=DEV)   # leave 256 MiB free
+    try:
+        got = system.ray_trace(fan, m0, m1, dtype="float32")               # needs 0.6 GB: the pool's memory
+        assert rt.history_buffers_held(0) == (0, 0)
+        assert torch.equal(got.cpu().view(torch.int32), want.view(torch.int32))
+        del got
+    finally:
+        del filler
+        torch.cuda.empty_cache()
+    assert E.device_empty((4,), torch.float32, DEV).numel() == 4
+
+
+def test_writer_streams_large_histories_back_to_back(tmp_path):
+    """The lightsheet pattern at scale (scripts/2024_04_01_lightsheet.py:51-60,134-135): >= 1 GiB default
+    histories (history buffers) written back to back through io.HistoryWriter, whose device-to-host copies
+    run on a side stream while the next configuration traces: every configuration reads back bitwise."""
+    from ray_trace_pb_amd import io as rio
+    import systems
+    C.check(C.lib().rtpb_buffer_trim())
+    system = systems.c3_system(rt, mat)
+    m0 = m1 = mat.Vacuum()
+    nt = nph = 1342                                         # 1,800,964 rays: 19 float32 planes = 1.02 GiB
+    fan = torch.empty((nt * nph, 8), dtype=torch.float64, device=DEV)
+    heights = [0.0, 5.0, 10.0, 15.0, 2.5]
+    P = 2 * len(system.surfaces) + 1
+    assert P * nt * nph * 8 * 4 >= rt.POOLED_HISTORY_BYTES
+    path = str(tmp_path / "sweep.zarr")
+    with rio.HistoryWriter(path, len(heights), P, nt * nph, dtype="float32") as w:
+        for k, h in enumerate(heights):
+            rt.fan_into(fan, np.array([h, 0, 0]), np.pi / 180, nt, 0.635, nph)
+            w.write(k, system.ray_trace(fan, m0, m1, dtype="float32"))
+    got = rio.read_array(path)
+    for k, h in enumerate(heights):
+        rt.fan_into(fan, np.array([h, 0, 0]), np.pi / 180, nt, 0.635, nph)
+        ref = torch.empty((P, nt * nph, 8), dtype=torch.float32, device=DEV)
+        system.ray_trace(fan, m0, m1, dtype="float32", out=ref)
+        assert np.array_equal(got[k].view(np.int32), ref.cpu().numpy().view(np.int32)), k
     C.check(C.lib().rtpb_buffer_trim())

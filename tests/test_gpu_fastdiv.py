@@ -45,6 +45,18 @@ def _check(a, a2, a3, b, kill):
         t = np.minimum(t1, t2)
         _same(out[26], np.where(t == np.inf, np.nan, t))
         _same(out[27], np.sign(a) * root)                       # RT:1217
+        # unit_or_zero (RT:1203-1209): exact form == NumPy's v / |v| with NaN -> 0; the trace kernels' fused
+        # form is identical wherever the norm squared is not NaN (a NaN norm leaves NaN: the surface's own
+        # on-surface test kills those rays)
+        v2 = a * a + a2 * a2 + a3 * a3
+        nrm2 = np.sqrt(v2)
+        for k, comp in enumerate((a, a2, a3)):
+            exp = comp / nrm2
+            exp = np.where(np.isnan(exp), 0.0, exp)
+            _same(out[31 + k], exp)
+            live = ~np.isnan(v2)
+            _same(out[28 + k][live], exp[live])
+            assert np.isnan(out[28 + k][~live]).all()
         # GuardDefer: no fallback branch; where the flag is clear the value is the exact one, and the
         # flag is set only where an operand left the shortcut's exact range (the flagged rays are re-traced)
         for val, flag, exp in ((out[9], out[10], a / b), (out[11], out[14], a / b), (out[12], out[14], a2 / b),
@@ -134,3 +146,20 @@ def test_fastdiv_normalisation_inputs():
     a = rng.uniform(-30, 30, n) * 10.0 ** rng.uniform(-16, 3, n)
     b = rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(-4, 4, n)
     _check(a, np.roll(a, 1), np.roll(a, 2), b, rng.random(n) < 0.05)
+
+
+def test_fused_norm_test_range_edges():
+    """unit_or_zero's combined test (norm2_fast: 2^-240 <= |v|^2 < 2^238 or NaN) straddled: vectors whose norm
+    squared lies just inside and outside both limits, with tiny, zero and huge companions -- the fused form
+    equals the exact one (and NumPy) bit for bit on every vector whose norm squared is a number."""
+    rng = np.random.default_rng(17)
+    n = 1 << 18
+    edge = np.where(rng.random(n) < 0.5, 2.0 ** -120, 2.0 ** 119) * (1.0 + rng.uniform(-1e-3, 1e-3, n))
+    edge *= np.where(rng.random(n) < 0.5, 1.0, 1.0 + np.ldexp(rng.integers(-4, 5, n).astype(float), -52))
+    a = edge * rng.choice([-1.0, 1.0], n)
+    a2 = np.where(rng.random(n) < 0.3, 0.0, a * rng.uniform(-1e-9, 1e-9, n))
+    a3 = np.where(rng.random(n) < 0.3, -0.0, np.ldexp(rng.uniform(0.5, 1.0, n), rng.integers(-1074, 600, n)))
+    a3[::97] = np.inf
+    a2[::89] = np.nan
+    kill = np.zeros(n, dtype=np.uint8)
+    _check(a, a2, a3, np.abs(a) + 1.0, kill)

@@ -56,3 +56,30 @@ def test_golden_cases_exercise_edge_semantics():
     assert miss.sum() > 0
     _, _, h = load_case("c4_opm")
     assert np.isnan(h[-1]).all(axis=1).sum() > 0              # NA clip of PerfectLens (RT:1757-1760)
+
+
+def test_ray_fan_rows_are_slices_of_the_whole_fan():
+    """oracle.ray_fan_rows (a fan traced in pieces, tests/oracle_pool.py) == the slice of ray_fan, bitwise."""
+    from oracle import rt_numpy as O
+    whole = O.ray_fan([0.3, -1.0, 2.0], 0.02, 37, 0.532, nphis=29)
+    for a, b in [(0, 29), (0, 1), (5, 17), (28, 29)]:
+        part = O.ray_fan_rows([0.3, -1.0, 2.0], 0.02, 37, 0.532, 29, a, b)
+        assert np.array_equal(part.view(np.int64), whole[a * 37:b * 37].view(np.int64))
+
+
+def test_oracle_pool_final_plane_equals_one_trace():
+    """The parallel oracle of the full-size C5 test equals one oracle trace of the whole fan (CPU, small)."""
+    import ray_trace_pb_amd.materials as mat
+    import ray_trace_pb_amd.raytrace as rt
+    import systems
+    from oracle import rt_numpy as O
+    from oracle_pool import fan_final_plane
+    from serialize import material_to_dict, surface_to_dict
+    system = systems.c5_system(rt, mat)
+    S = [surface_to_dict(s) for s in system.surfaces]
+    M = [material_to_dict(m) for m in [mat.Constant(1)] + list(system.materials) + [mat.Constant(1)]]
+    field = systems.c5_field_points(8)[9]
+    theta = 0.5 * np.pi / 180
+    got = fan_final_plane(S, M, field, theta, 41, 0.561, 23, procs=3, rows_per_piece=4)
+    ref = O.ray_trace(S, M, O.ray_fan(field, theta, 41, 0.561, nphis=23))[-1]
+    assert np.array_equal(got.view(np.int64), ref.view(np.int64))

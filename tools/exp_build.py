@@ -1,6 +1,6 @@
 """Build an EXPERIMENT variant of librtpb.so from a patched scratch copy of the sources: the shipped
 sources carry no experiment branches.  Applies the given patches (-p1, repository-relative paths) and
-compiles with the given -D flags.  Never shipped: used by tools/ab_variants.py / tools/ab_libs.py to find
+compiles with the given -D flags.  Never shipped: used by tools/ab_variants.py to find
 where kernel time goes.  Named variants with reviewable source edits: tools/exp_variants.py.  The round-2
 switches (RTPB_EXP_NO_COMPUTE, XCD_REMAP, PERSIST, ...) are profiles/r02/experiments/experiments_round2.patch,
 which applies to the round-2 sources (commit 7b1cac3).

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--flag", type=int, default=4, help="hipExtMallocWithFlags flags (4 = contiguous)")
     ap.add_argument("--kinds", default="contig,torch",
-                    help="contig (hipDeviceMallocContiguous), torch, sN (chunks of N MiB mapped in shuffled order)")
+                    help="contig (hipDeviceMallocContiguous), torch, sN (history_buffer: chunks of N MiB mapped in shuffled order)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -42,19 +42,7 @@ def main():
     P = len(sel)
     lo, hi = E.plane_mask(sel)
     nbytes = P * n * 32
-    bufs, raw, scattered = {}, [], []
-    sc = None
-    if any(k.startswith("s") for k in args.kinds.split(",")):
-        import subprocess
-        so = os.path.join(ROOT, "tools", "_build", "libscatter_alloc.so")
-        if not os.path.exists(so):
-            os.makedirs(os.path.dirname(so), exist_ok=True)
-            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC", "-o", so,
-                            os.path.join(ROOT, "tools", "scatter_alloc.hip")], check=True)
-        sc = ctypes.CDLL(so)
-        sc.scatter_alloc.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
-                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]
-        sc.scatter_free.argtypes = [ctypes.c_void_p]
+    bufs, raw = {}, []
     import time
     for k in range(args.pairs):
         for kind in args.kinds.split(","):
@@ -70,13 +58,8 @@ def main():
             elif kind == "torch":
                 bufs[f"torch{k}"] = torch.empty((P, n, 8), dtype=torch.float32, device=dev)
             else:
-                p, hd = ctypes.c_void_p(), ctypes.c_void_p()
-                rc = sc.scatter_alloc(0, nbytes, int(kind[1:]) << 20, 1000 + k, ctypes.byref(p), ctypes.byref(hd))
-                if rc != 0:
-                    print(f"scatter_alloc({kind}) failed: {rc}", flush=True)
-                else:
-                    bufs[f"{kind}_{k}"] = p.value
-                    scattered.append(hd.value)
+                # the product's history buffer (rtpb_buffer_alloc) with N MiB chunks in shuffled order
+                bufs[f"{kind}_{k}"] = E.history_buffer((P, n, 8), torch.float32, dev, chunk_bytes=int(kind[1:]) << 20)
             torch.cuda.synchronize()
             print(f"alloc {kind}{k}: {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
     h = ctypes.c_void_p()
@@ -108,8 +91,6 @@ def main():
         print(f"{name:10s} ms={np.median(times[name]):.4f} ({', '.join(f'{t:.3f}' for t in times[name])})", flush=True)
     for p in raw:
         hip.hipFree(p)
-    for hd in scattered:
-        sc.scatter_free(hd)
 
 
 if __name__ == "__main__":
