@@ -216,6 +216,8 @@ RTPB_HD T np_sign(T v) {
 //   ((x - 0) * 0 + (y - 0) * 0) + (z - cz) * 1  ==  fma(y, 0, x * 0) + (z - cz)      (5 -> 3 float64 ops)
 // The specialised surface steps (surface_step<..., AX = true>) use only these identities.
 constexpr int32_t kAxial = 64;
+// rcp_ok bit 7: a PerfectLens with 2^-80 <= |focal_len| < 2^120, so -|r1| / f is inside the shortcut range
+constexpr int32_t kLensQ1 = 128;
 
 RTPB_HD double tfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
@@ -329,12 +331,14 @@ __device__ __forceinline__ Rcp<double> make_rcp_in_range(double b) {
 #endif
 
 // a / r.b
-template <typename T, class G = GuardBranch>
+// NUM_IN_RANGE: the caller guarantees the numerator is 0, inf, NaN or 2^-800 <= |a| <= 2^600 (see
+// norm_quotient_bound), so only the divisor's range is tested
+template <typename T, class G = GuardBranch, bool NUM_IN_RANGE = false>
 RTPB_HD T div1(T a, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, r.b, r.y);
-        const bool num_ok = fastdiv_num_ok(a);
+        const bool num_ok = NUM_IN_RANGE || fastdiv_num_ok(a);
         const bool slow = !(r.ok & num_ok);     // bitwise: no short-circuit branch around the fast path
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
@@ -350,12 +354,12 @@ RTPB_HD T div1(T a, const Rcp<T>& r, G* g = nullptr) {
 
 // a / b where r = make_rcp(b0) and b is b0 or NaN (a wavelength after its row was killed): a NaN b gives
 // NaN either way (div_fixup / the division), so y of b0 serves every value b can take
-template <typename T, class G = GuardBranch>
+template <typename T, class G = GuardBranch, bool NUM_IN_RANGE = false>
 RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
         T q = fastdiv_q(a, b, r.y);
-        const bool num_ok = fastdiv_num_ok(a);
+        const bool num_ok = NUM_IN_RANGE || fastdiv_num_ok(a);
         const bool slow = !(r.ok & num_ok);     // bitwise: no short-circuit branch around the fast path
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
@@ -368,6 +372,12 @@ RTPB_HD T div1_as(T a, T b, const Rcp<T>& r, G* g = nullptr) {
     (void)g;
     return a / b;
 }
+
+// Numerators bounded by construction.  A Euclidean norm RN(sqrt(v)), v a sum of squares, is 0, +inf, NaN or
+// between sqrt(2^-1074) = 2^-537 and sqrt(DBL_MAX) < 2^512; its product with 2 pi (the phase updates'
+// distance terms, RT:297 / RT:1512) lies in [2^-535, 2^515], and its quotient by a focal length with
+// 2^-80 <= |f| < 2^120 (PerfectLens sin_t2, RT:1749) in [2^-657, 2^592] -- all inside the exact range of the
+// shortcut quotients (2^-800 <= |a| <= 2^600), so those divisions test the divisor only (NUM_IN_RANGE).
 
 // The per-ray divisor of every phase update (the wavelength) with 2 pi / wl once per ray
 template <typename T, class G = GuardBranch>
@@ -514,7 +524,7 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
     // dist * s * 2 * pi (RT:297): s = +-1 is a sign, and 2 * pi is exact, so ((d s) 2) pi == (+-d) (2 pi)
     // bit for bit -- the two real products are the same number (overflow to inf included)
-    o.ph = r.ph + div1_as((s < T(0) ? -dist : dist) * T(Const<T>::two_pi), r.wl, iwl, g) * n;
+    o.ph = r.ph + div1_as<T, G, true>((s < T(0) ? -dist : dist) * T(Const<T>::two_pi), r.wl, iwl, g) * n;
     o.wl = r.wl;
     kill_if(exclude_backward && s == T(-1), o);
     if (t_out) *t_out = t;
@@ -550,7 +560,7 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
     const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
     const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz, g);
-    o.ph = r.ph + div1_as(dist * T(Const<T>::two_pi), r.wl, iwl, g) * n;     // == (d 2) pi, see to_plane
+    o.ph = r.ph + div1_as<T, G, true>(dist * T(Const<T>::two_pi), r.wl, iwl, g) * n;  // == (d 2) pi, see to_plane
     o.wl = r.wl;
     return o;
 }
@@ -565,19 +575,20 @@ RTPB_HD bool positive_finite(T v) {
 }
 
 // v / |v| with NaN components replaced by 0 (RT:1203-1209)
-// FUSED (the trace kernels' own surface steps): a NaN norm -- a NaN or infinite component of d x N or N x b,
-// i.e. a NaN / infinite direction or normal -- leaves NaN quotients instead of zeros.  Every such ray is
-// killed by the surface's own on-surface test in the same step (its intersection is NaN or infinite: the
-// direction entered the intersection, and a sphere's normal is NaN only where its intersection is), so the
-// stored values are the same; the user-geometry kernels (rtpb_interact, normals from user code) keep the
-// exact fix-ups.  A finite in-range norm squared takes the combined test (norm2_fast) instead of three.
-template <bool FUSED = false, typename T, class G = GuardBranch>
+// Device: a norm squared in [2^-240, 2^238) or NaN takes one combined range test (norm2_fast) instead of the
+// square root's, the divisor's and the class test of the NaN fix-ups: an in-range norm is positive and finite
+// (no quotient can be NaN), and a NaN norm makes every quotient NaN, i.e. every component 0.  The rest (0,
+// tiny, huge, infinite norms) takes the full sequences below.
+template <typename T, class G = GuardBranch>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 #if defined(RTPB_FASTNORM)
-    if constexpr (FUSED && sizeof(T) == 8 && !G::kDefer) {
+    if constexpr (sizeof(T) == 8 && !G::kDefer) {
         const T v = x * x + y * y + z * z;
         if (__builtin_expect(norm2_fast(v), 1)) {
             div3_norm(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
+            if (__builtin_expect(v != v, 0)) {
+                x = T(0); y = T(0); z = T(0);
+            }
             return;
         }
     }
@@ -596,7 +607,7 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
 // AX: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot)
-template <bool AX = false, bool FUSED = false, typename T, class G = GuardBranch>
+template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
     T bx, by, bz;
     if constexpr (AX) {
@@ -608,7 +619,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         by = ri.dz * Nx - ri.dx * Nz;
         bz = ri.dx * Ny - ri.dy * Nx;
     }
-    unit_or_zero<FUSED>(bx, by, bz, g);
+    unit_or_zero(bx, by, bz, g);
     if constexpr (AX) {
         cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
         cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
@@ -618,7 +629,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         cy = Nz * bx - Nx * bz;
         cz = Nx * by - Ny * bx;
     }
-    unit_or_zero<FUSED>(cx, cy, cz, g);
+    unit_or_zero(cx, cy, cz, g);
 }
 
 // np.sign(v) * root for root >= +0 or NaN (RT:1217; 1 - m^2 is never -0): for v < 0 or v > 0 the product is
@@ -633,10 +644,10 @@ RTPB_HD T signed_root(T v, T root) {
 // Snell refraction of the intersected ray (RT:1197-1221)
 // ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
 // AX: N == (+0, +0, 1) (axdot)
-template <bool AX = false, bool FUSED = false, typename T, class G = GuardBranch>
+template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis<AX, FUSED>(ri, Nx, Ny, Nz, cx, cy, cz, g);
+    tangent_basis<AX>(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
     const T tang = signed_root(axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz), tsqrt<T>(T(1) - mag * mag, g));
     Ray<T> o;
@@ -659,10 +670,10 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr
 }
 
 // law of reflection (RT:1267-1289)
-template <bool FUSED = false, typename T, class G = GuardBranch>
+template <typename T, class G = GuardBranch>
 RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
     T cx, cy, cz;
-    tangent_basis<false, FUSED>(ri, Nx, Ny, Nz, cx, cy, cz, g);
+    tangent_basis(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag_na = -(Nx * ri.dx + Ny * ri.dy + Nz * ri.dz);
     const T mag_nc = cx * ri.dx + cy * ri.dy + cz * ri.dz;
     Ray<T> o;
@@ -772,11 +783,14 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         o.x = h * spx + Bx;
         o.y = h * spy + By;
         o.z = h * spz + Bz;
-        const T q1 = div1(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
+        // -r1n is a norm (bounded, see NUM_IN_RANGE); with 2^-80 <= |f| < 2^120 (host bit kLensQ1) so is q1 =
+        // -r1n / f: 2^-657 <= |q1| <= 2^592, or 0, inf, NaN
+        const T q1 = div1<T, G, true>(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
         T sin_t2;
         if (s.rcp_ok & 8) {
             RTPB_NO_SPECULATE();
-            sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
+            if (s.rcp_ok & kLensQ1) sin_t2 = div1<T, G, true>(q1, host_rcp(n2, s.rn2, true), g);
+            else sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
         } else {
             sin_t2 = q1 / n2;
         }
@@ -821,7 +835,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
-            after = reflect<true>(ri, Nx, Ny, Nz, g);
+            after = reflect(ri, Nx, Ny, Nz, g);
             kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
@@ -834,7 +848,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             } else {
                 ratio = n1 / n2;
             }
-            after = snell<AX && KIND == FLAT, true>(ri, Nx, Ny, Nz, ratio, g);
+            after = snell<AX && KIND == FLAT>(ri, Nx, Ny, Nz, ratio, g);
             const bool ok = (KIND == SPHERE) ? on_sphere<AX>(ri, s) : on_flat<AX>(ri, s);
             kill_if(!ok, after);
         }
@@ -998,6 +1012,8 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     else if (d.kind == SPHERE) axial = on_axis && z_axis(s.input_axis) && d.shell_hi < HUGE_VAL;
     else if (d.kind == PERFECT_LENS) axial = on_axis && z_axis(s.normal);
     if (axial) d.rcp_ok |= kAxial;
+    if (d.kind == PERFECT_LENS && std::fabs(s.focal_len) >= 0x1p-80 && std::fabs(s.focal_len) < 0x1p120)
+        d.rcp_ok |= kLensQ1;
     d.nr = 0.0;
     d.rn2 = 0.0;
     return d;

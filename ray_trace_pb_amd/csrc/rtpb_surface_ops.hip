@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kTraceBlock) void interact_kernel(HookArgs a) {
         const double Nx = nv[0], Ny = nv[1], Nz = nv[2];
         Ray<double> o;
         if (a.mode == RTPB_REFLECT) {
-            o = reflect<false>(h, Nx, Ny, Nz);                                      // RT:1266-1289
+            o = reflect<double>(h, Nx, Ny, Nz);                                      // RT:1266-1289
         } else {
             const cptr<DevMaterial<double>> mp = (cptr<DevMaterial<double>>)(a.mats);
             const double n1 = material_n<double>(load_material<double>(mp), h.wl, a.table);

@@ -14,7 +14,7 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kOut = 34;
+constexpr int kOut = 32;
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
@@ -23,8 +23,8 @@ constexpr int kOut = 34;
 //      [11..13] div3, [14] its flag, [15] tsqrt(b), [16] its flag, [17] div1_as, [18] its flag,
 //      [19..21] div3_norm((a, a2, a3), rcp(their norm)), [22..24] its GuardDefer form, [25] that flag,
 //      [26] sphere_root(B = a, root = tsqrt(|b|)), [27] signed_root(a, tsqrt(|b|)),
-//      [28..30] unit_or_zero<FUSED>(a, a2, a3) (the trace kernels' combined norm test), [31..33] the exact
-//      unit_or_zero (NaN components of the quotient replaced by 0)
+//      [28..30] unit_or_zero(a, a2, a3) (the combined norm test, NaN components of the quotient replaced by 0),
+//      [31] the phase term |(a, a2, a3)| * 2 pi / b with the numerator's range implied (div1_as NUM_IN_RANGE)
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -75,15 +75,12 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[26 * n + i] = sphere_root(ai, rt);
     out[27 * n + i] = signed_root(ai, rt);
     double fx = ai, fy = a2[i], fz = a3[i];
-    unit_or_zero<true>(fx, fy, fz);
+    unit_or_zero(fx, fy, fz);
     out[28 * n + i] = fx;
     out[29 * n + i] = fy;
     out[30 * n + i] = fz;
-    double ex = ai, ey = a2[i], ez = a3[i];
-    unit_or_zero<false>(ex, ey, ez);
-    out[31 * n + i] = ex;
-    out[32 * n + i] = ey;
-    out[33 * n + i] = ez;
+    const double dist = tsqrt<double>(ai * ai + a2[i] * a2[i] + a3[i] * a3[i]);
+    out[31 * n + i] = div1_as<double, GuardBranch, true>(dist * Const<double>::two_pi, bi, r);
 }
 
 }  // namespace
