@@ -315,10 +315,11 @@ RTPB_HD Rcp<T> make_rcp(T b) {
 // fastdiv_den_ok -- so ONE test on v (its high word: the bounds have zero low words) replaces the square
 // root's class / high-word test and the divisor's frexp test.  NaN v also takes the fast path (the core,
 // the reciprocal and the quotients all give NaN, as the full sequences do).
-__device__ __forceinline__ bool norm2_fast(double v) {
+__device__ __forceinline__ bool norm2_in_range(double v) {
     const uint32_t hi = static_cast<uint32_t>(__double2hiint(v));
-    return (hi - 0x30F00000u < 0x4ED00000u - 0x30F00000u) | (v != v);
+    return hi - 0x30F00000u < 0x4ED00000u - 0x30F00000u;
 }
+__device__ __forceinline__ bool norm2_fast(double v) { return norm2_in_range(v) | (v != v); }
 
 // make_rcp for a divisor known to be in range (or NaN): the same instructions without the test
 __device__ __forceinline__ Rcp<double> make_rcp_in_range(double b) {
@@ -575,20 +576,17 @@ RTPB_HD bool positive_finite(T v) {
 }
 
 // v / |v| with NaN components replaced by 0 (RT:1203-1209)
-// Device: a norm squared in [2^-240, 2^238) or NaN takes one combined range test (norm2_fast) instead of the
-// square root's, the divisor's and the class test of the NaN fix-ups: an in-range norm is positive and finite
-// (no quotient can be NaN), and a NaN norm makes every quotient NaN, i.e. every component 0.  The rest (0,
-// tiny, huge, infinite norms) takes the full sequences below.
+// Device: a norm squared in [2^-240, 2^238) takes one range test (norm2_in_range) instead of the square
+// root's, the divisor's and the class test of the NaN fix-ups -- the norm is then positive and finite, so no
+// quotient can be NaN.  The rest (0, tiny, huge, infinite and NaN norms: normal incidence, dead rows) takes
+// the full sequences and fix-ups below.
 template <typename T, class G = GuardBranch>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 #if defined(RTPB_FASTNORM)
     if constexpr (sizeof(T) == 8 && !G::kDefer) {
         const T v = x * x + y * y + z * z;
-        if (__builtin_expect(norm2_fast(v), 1)) {
+        if (__builtin_expect(norm2_in_range(v), 1)) {
             div3_norm(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
-            if (__builtin_expect(v != v, 0)) {
-                x = T(0); y = T(0); z = T(0);
-            }
             return;
         }
     }
