@@ -98,6 +98,16 @@ template <typename T> RTPB_HD bool is_nan(T v) { return v != v; }
 #define RTPB_FASTSQRT 1
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// A class-test mask as a scalar register: v_cmp_class_f64 then takes it as an SGPR operand (VOP3) instead of
+// a VGPR the compiler rematerialises with a v_mov (one VALU per test) when registers are tight.
+__device__ __forceinline__ int class_mask(int k) {
+    int r;
+    asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
+    return r;
+}
+#endif
+
 // Guard policies of the exact fast paths below.  Each shortcut is exact only inside a range of its
 // operands; outside it the operation must take the compiler's full sequence.
 //   GuardBranch: a per-operation branch to the full sequence (default; the all-planes history kernels).
@@ -140,7 +150,7 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     // the set -- +-0, +denormals, +normals below 2^-767, +inf -- as one class test and one 32-bit
     // compare of the high word (negative values and NaN have it at or above 0x10000000 unsigned)
     // (bitwise |: both tests are one VALU each; a short-circuit || puts the core under a branch of its own)
-    const bool special = __builtin_amdgcn_class(v, 0x2E0);
+    const bool special = __builtin_amdgcn_class(v, class_mask(0x2E0));
     const bool slow = special | (static_cast<uint32_t>(__double2hiint(v)) < 0x10000000u);
     if constexpr (G::kDefer) {
         // +-0 and +inf (normal incidence gives sqrt(0) on every axial ray) are their own square roots:
@@ -196,7 +206,7 @@ RTPB_HD void kill_if(bool c, Ray<T>& r) {
 template <typename T>
 RTPB_HD bool nonneg_finite(T v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, 0x1E0);    // -0 | +0 | +denormal | +normal
+    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, class_mask(0x1E0));  // -0 | +0 | +denorm | +normal
 #endif
     return v >= T(0) && v < T(1) / T(0);
 }
@@ -544,6 +554,13 @@ RTPB_HD T sphere_root(T B, T root) {
     const T t1 = T(0.5) * (-B + root);
     const T t2 = T(0.5) * (-B - root);
     T t = t2 >= T(0) ? t2 : t1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(T) == 8) {
+        // the NaN's high word from a scalar register (a VOP2 select's first operand), not a VGPR constant
+        if (!nonneg_finite(t)) t = __hiloint2double(class_mask(0x7FF80000), 0);
+        return t;
+    }
+#endif
     if (!nonneg_finite(t)) t = qnan<T>();
     return t;
 }
@@ -570,7 +587,7 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
 template <typename T>
 RTPB_HD bool positive_finite(T v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, 0x180);    // +denormal | +normal
+    if constexpr (sizeof(T) == 8) return __builtin_amdgcn_class(v, class_mask(0x180));  // +denormal | +normal
 #endif
     return v > T(0) && v < T(1) / T(0);
 }
