@@ -21,6 +21,7 @@ What runs where
   7-9, 11-12).
 """
 import functools
+import threading
 from collections.abc import Sequence
 from copy import deepcopy
 from typing import Optional
@@ -462,6 +463,23 @@ def _default_history(code, last, sel, layout_code):
     return E.history_buffer(shape, torch.float64 if elem == 8 else torch.float32, last.device)
 
 
+_MISS_FLAGS = threading.local()
+
+
+def _miss_flag(device):
+    """The table-miss flag of rtpb_trace_checked for this thread and device: one int32 in pinned host memory,
+    which the kernel writes directly (a miss is rare) and the host reads after synchronising the launch
+    stream -- no device allocation, fill or device-to-host copy per call."""
+    import torch
+    flags = getattr(_MISS_FLAGS, "flags", None)
+    if flags is None:
+        flags = _MISS_FLAGS.flags = {}
+    f = flags.get(device)
+    if f is None:
+        f = flags[device] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    return f
+
+
 def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out=None):
     """The torch-CUDA trace of trace_surfaces.  Tabulated materials (user n() overrides, Ebaf11) are
     lowered with the key set of the previous bundle traced through them when there is one, and the kernel
@@ -488,9 +506,11 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layou
     fp = E.table_fingerprint(tab)
     prev = E.previous_keys(fp)
     if prev is not None:
-        miss = torch.zeros(1, dtype=torch.int32, device=last.device)
+        miss = _miss_flag(last.device)
+        miss[0] = 0
         res = run(E.lower(surfaces, materials, lambda: prev, code), miss)
-        if int(miss.item()) == 0:
+        torch.cuda.current_stream(last.device).synchronize()       # the launch has set the flag or not
+        if int(miss[0]) == 0:
             return res
         del res
     keys = E.distinct_wavelengths(last[:, 7])

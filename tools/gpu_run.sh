@@ -18,7 +18,8 @@
 #   pmc_c5           PMC passes of the fused C5 sweep kernel (1 field)
 #   e2e              host phases of the drop-in call (tools/e2e_phases.py)
 #   power            socket power / clock under the history kernels (tools/power_probe.py)
-#   ab:LIB           A/B of the in-tree library against LIB (tools/ab_variants.py, histories + C5 sweep)
+#   ab:LIB[,LIB..]   A/B of the in-tree library against experiment builds (tools/ab_variants.py, histories;
+#                    C5 sweep per library, the in-tree one before and after)
 #   py:SCRIPT[:ARGS] python3 tools/SCRIPT.py ARGS (ARGS with ',' for spaces)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -61,10 +62,13 @@ for s in "$@"; do
         step "power_$(echo $args | tr -c 'a-z0-9' '_')" 120 python3 tools/power_probe.py $args --seconds 6
       done ;;
     ab:*)
-      lib="${s#ab:}"
-      step ab_hist 900 python3 tools/ab_variants.py --libs "$lib" --configs c4:1.0,c3:1.0,c2 --modes all,final --rounds 5 --reps 3
+      libs="${s#ab:}"
+      step ab_hist 900 python3 tools/ab_variants.py --libs "$libs" --configs c4:1.0,c3:1.0,c2 --modes all,final --rounds 5 --reps 3
       step c5_new 300 python3 tools/c5_sweep.py
-      step c5_ab 300 python3 tools/c5_sweep.py --lib "$lib" ;;
+      for lib in $(echo "$libs" | tr ',' ' '); do
+        step "c5_$(basename "$lib" .so)" 300 python3 tools/c5_sweep.py --lib "$lib"
+      done
+      step c5_new_again 300 python3 tools/c5_sweep.py ;;
     py:*)
       spec="${s#py:}"; script="${spec%%:*}"; args=""
       [ "$spec" != "$script" ] && args="$(echo "${spec#*:}" | tr ',' ' ')"
