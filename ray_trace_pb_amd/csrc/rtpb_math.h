@@ -604,8 +604,16 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
         const T v = x * x + y * y + z * z;
         if (__builtin_expect(norm2_in_range(v), 1)) {
             div3_norm(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
-            return;
+        } else {
+            // the compiler's correctly rounded sqrt and divisions (one straight sequence: compact code for the
+            // rare lanes), then the reference's NaN -> 0
+            const T nrm = sqrt(v);
+            x = x / nrm; y = y / nrm; z = z / nrm;
+            if (is_nan(x)) x = T(0);
+            if (is_nan(y)) y = T(0);
+            if (is_nan(z)) z = T(0);
         }
+        return;
     }
 #endif
     const T nrm = tsqrt<T>(x * x + y * y + z * z, g);
@@ -774,15 +782,19 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
                 const T spn = sqrt_core(spv);
                 if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp_in_range(spn), g);
             } else {
-                const T spn = tsqrt<T>(spv, g);
-                if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
+                const T spn = sqrt(spv);                              // the compiler's full sequences
+                if (spn > T(1e-12)) {
+                    spx = spx / spn; spy = spy / spn; spz = spz / spn;
+                }
             }
             if (__builtin_expect(norm2_fast(r1v), 1)) {
                 r1n = sqrt_core(r1v);
                 div3_norm(ux, uy, uz, make_rcp_in_range(r1n), g);     // r1n >= 2^-120 or NaN: != 0
             } else {
-                r1n = tsqrt<T>(r1v, g);
-                if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
+                r1n = sqrt(r1v);
+                if (r1n != T(0)) {
+                    ux = ux / r1n; uy = uy / r1n; uz = uz / r1n;
+                }
             }
         } else
 #endif
