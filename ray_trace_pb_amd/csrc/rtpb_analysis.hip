@@ -174,17 +174,36 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
     };
     double n_cur = mat_n(0);
-    for (int s = 0; s < a.nsurf; ++s) {
-        const double n_next = mat_n(s + 1);
-        DevSurface<double> sd = load_surface<double>(surf + s);
-        if constexpr ((FEAT & 16) != 0) {
-            // the group's media are uniform: the Snell ratio and 1 / n2 from the host (IEEE division)
-            sd.nr = gn[a.nsurf + 1 + s];
-            sd.rn2 = gn[2 * a.nsurf + 1 + s];
-            sd.rcp_ok = (sd.rcp_ok & ~(4 | 8)) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
-        }
-        propagate_surface_multi<double, (FEAT & 1) != 0, kSweepRays>(sd, r, n_cur, n_next, iwl);
-        n_cur = n_next;
+    // runs of consecutive surfaces of one (kind, axial) code: each run loops inside one instantiation of the
+    // surface step, so the rays' registers carry from surface to surface without the copies a per-surface
+    // join of the kind branches needs (the ODT path of C5: 12 axial spheres, a lens, a flat = 3 runs)
+    auto code_of = [&](int k) { return surface_code<double>((surf + k)->kind, (surf + k)->rcp_ok); };
+    int s = 0;
+    while (s < a.nsurf) {
+        const int code = code_of(s);
+        dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
+            constexpr int K = decltype(kind)::value;
+            constexpr bool A = decltype(ax)::value;
+            do {
+                const double n_next = mat_n(s + 1);
+                DevSurface<double> sd = load_surface<double>(surf + s);
+                if constexpr ((FEAT & 16) != 0) {
+                    // the group's media are uniform: the Snell ratio and 1 / n2 from the host (IEEE division)
+                    sd.nr = gn[a.nsurf + 1 + s];
+                    sd.rn2 = gn[2 * a.nsurf + 1 + s];
+                    sd.rcp_ok = (sd.rcp_ok & ~(4 | 8)) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
+                }
+                auto none = [](const Ray<double>&) {};
+                Ray<double> o[kSweepRays];
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q)
+                    surface_step<double, K, A>(sd, r[q], n_cur, n_next, iwl, none, o[q]);
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q) r[q] = o[q];
+                n_cur = n_next;
+                ++s;
+            } while (s < a.nsurf && code_of(s) == code);
+        });
     }
     auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
         double v[kStats] = {0, 0, 0, 0, 0, 0, 0};

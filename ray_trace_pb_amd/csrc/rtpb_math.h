@@ -908,6 +908,42 @@ RTPB_HD void dispatch_kind(const DevSurface<T>& s, Step&& step) {
     }
 }
 
+// The (kind, kAxial) pair of dispatch_kind as one integer, and the dispatch on it: a loop can run a whole RUN
+// of consecutive surfaces of one code inside one instantiation of the step (no per-surface join of the kind
+// branches, so the ray's registers carry over from surface to surface without copies)
+template <typename T>
+RTPB_HD int surface_code(int kind, int32_t rcp_ok) {
+    return 2 * kind + ((rcp_ok & kAxial) != 0 && kind != PLANE_MIRROR ? 1 : 0);
+}
+
+template <bool WITH_LENS, typename Step>
+RTPB_HD void dispatch_code(int code, Step&& step) {
+    using std::integral_constant;
+    switch (code) {
+    case 2 * PERFECT_LENS + 1:
+        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, true>()); break; }
+        [[fallthrough]];
+    case 2 * FLAT + 1:
+        step(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+        break;
+    case 2 * SPHERE + 1:
+        step(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
+        break;
+    case 2 * SPHERE:
+        step(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+        break;
+    case 2 * PLANE_MIRROR:
+        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<bool, false>());
+        break;
+    case 2 * PERFECT_LENS:
+        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, false>()); break; }
+        [[fallthrough]];
+    default:
+        step(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+        break;
+    }
+}
+
 template <typename T, bool WITH_LENS = true, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
                                     EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
