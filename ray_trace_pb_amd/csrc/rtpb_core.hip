@@ -113,6 +113,11 @@ std::vector<unsigned char> build_blob(const rtpb_plan& p) {
         o.rR = T(d.rR); o.rf = T(d.rf); o.rcp_ok = d.rcp_ok;
         for (int j = 0; j < 3; ++j) o.nf[j] = T(d.nf[j]);
         o.nr = T(d.nr); o.rn2 = T(d.rn2);
+        for (int j = 0; j < 3; ++j) {
+            o.lF[j] = T(d.lF[j]);
+            o.lB[j] = T(d.lB[j]);
+        }
+        o.ln1f = T(d.ln1f); o.lph = T(d.lph);
     }
     auto* dm = reinterpret_cast<DevMaterial<T>*>(blob.data() + off_mats);
     for (size_t k = 0; k < M; ++k) dm[k] = device_material(p, k);

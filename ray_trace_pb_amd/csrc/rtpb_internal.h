@@ -115,6 +115,11 @@ __device__ __forceinline__ DevSurface<T> load_surface(cptr<DevSurface<T>> p) {
     d.rR = p->rR; d.rf = p->rf;
     d.nf[0] = p->nf[0]; d.nf[1] = p->nf[1]; d.nf[2] = p->nf[2];
     d.nr = p->nr; d.rn2 = p->rn2;
+    for (int j = 0; j < 3; ++j) {
+        d.lF[j] = p->lF[j];
+        d.lB[j] = p->lB[j];
+    }
+    d.ln1f = p->ln1f; d.lph = p->lph;
     return d;
 }
 

@@ -69,6 +69,13 @@ struct DevSurface {
     // rounded values the per-lane divisions give)
     T nr;
     T rn2;
+    // PerfectLens between uniform media (rcp_ok bit kLensUni; kLensUniVac: valid where Vacuum's n is 1): the focal
+    // points F = C - (n f) n1 and B = C + (n f) n2 (RT:1682-1687), n1 f (RT:1755) and the phase term
+    // n1 n1 f + n2 n2 f (RT:1776-1777), evaluated on the host in the kernel's order
+    T lF[3];
+    T lB[3];
+    T ln1f;
+    T lph;
 };
 
 template <typename T>
@@ -228,6 +235,16 @@ RTPB_HD T np_sign(T v) {
 constexpr int32_t kAxial = 64;
 // rcp_ok bit 7: a PerfectLens with 2^-80 <= |focal_len| < 2^120, so -|r1| / f is inside the shortcut range
 constexpr int32_t kLensQ1 = 128;
+// rcp_ok bits 8 / 9: a PerfectLens between uniform media whose focal points and constants come from the descriptor
+// (lF, lB, ln1f, lph); bit 9 = the same next to a Vacuum, valid when every ray of the wave has an ordinary
+// wavelength (the trace kernel turns it into bit 8).  On a kAxial lens the host sets them only when F and B lie on
+// the axis bit for bit (x, y = +0), so the focal-plane propagation takes the axial form too.
+constexpr int32_t kLensUni = 256;
+constexpr int32_t kLensUniVac = 512;
+// rcp_ok bits 10 / 11: the radius is positive / negative, finite and in the shortcut divisor range (a sphere normal's
+// quotients then need no div_fixup, fastdiv_q_nofix)
+constexpr int32_t kRPos = 1024;
+constexpr int32_t kRNeg = 2048;
 
 RTPB_HD double tfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
@@ -289,6 +306,26 @@ __device__ __forceinline__ double fastdiv_q(double a, double b, double y) {
     const double q0 = a * y;
     const double e = __builtin_fma(-b, q0, a);
     return __builtin_amdgcn_div_fixup(__builtin_fma(e, y, q0), b, a);
+}
+// The same quotient without div_fixup, for a divisor of known sign (SIGN = +1: b > 0, -1: b < 0) in the shortcut
+// range and a FINITE numerator in range (NaN is fine too: it propagates).  For such operands div_fixup only
+// re-applies sign(a) ^ sign(b) to |q| (the special-value cases -- b = 0 / inf / NaN, a = inf, quotient
+// under/overflow -- cannot occur), and q already carries that sign unless a = +-0.  For a zero numerator the
+// residual is an exact +0, so the sign of the correction's zero product decides: with the residual taken as
+// -(a - b q0) = fma(b, q0, -a) and subtracted, the product -0 * y is -0 for y > 0; with a - b q0 added, +0 * y
+// is -0 for y < 0 -- either way q0 (which has the right sign) survives the final addition.  Non-zero results
+// are RN(q0 + (a - b q0) y), the fixup sequence's value bit for bit.
+template <int SIGN>
+__device__ __forceinline__ double fastdiv_q_nofix(double a, double b, double y) {
+    static_assert(SIGN == 1 || SIGN == -1, "divisor sign");
+    const double q0 = a * y;
+    if constexpr (SIGN > 0) {
+        const double e = __builtin_fma(b, q0, -a);
+        return __builtin_fma(-e, y, q0);
+    } else {
+        const double e = __builtin_fma(-b, q0, a);
+        return __builtin_fma(e, y, q0);
+    }
 }
 #endif
 
@@ -427,11 +464,14 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 // bound of the exact range (frexp exponent >= -799; 0, inf and NaN give 0): one min3 for the three instead
 // of three two-sided tests.  A norm of 0, inf or NaN is in r.ok's range and div_fixup returns the IEEE
 // quotient for those divisors whatever the numerator.
-template <typename T, class G = GuardBranch>
+// SIGN = +1 / -1: the divisor is known positive / negative and the numerators finite wherever the result matters
+// (fastdiv_q_nofix: no div_fixup); 0: any divisor and numerator (div_fixup).
+template <typename T, class G = GuardBranch, int SIGN = 0>
 RTPB_HD void div3_norm(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
-        const T qx = fastdiv_q(x, r.b, r.y), qy = fastdiv_q(y, r.b, r.y), qz = fastdiv_q(z, r.b, r.y);
+        auto q = [&](T a) { if constexpr (SIGN == 0) return fastdiv_q(a, r.b, r.y); else return fastdiv_q_nofix<SIGN>(a, r.b, r.y); };
+        const T qx = q(x), qy = q(y), qz = q(z);
         const int e = std::min(std::min(__builtin_amdgcn_frexp_exp(x), __builtin_amdgcn_frexp_exp(y)),
                                __builtin_amdgcn_frexp_exp(z));
         const bool slow = !(r.ok & (e >= -799));
@@ -603,7 +643,8 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
     if constexpr (sizeof(T) == 8 && !G::kDefer) {
         const T v = x * x + y * y + z * z;
         if (__builtin_expect(norm2_in_range(v), 1)) {
-            div3_norm(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
+            // positive norm, finite components: the quotients need no div_fixup
+            div3_norm<T, G, 1>(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
         } else {
             // the compiler's correctly rounded sqrt and divisions (one straight sequence: compact code for the
             // rare lanes), then the reference's NaN -> 0
@@ -739,6 +780,111 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
     }
 }
 
+// ------------------------------------------------------------------ PerfectLens (RT:1558-1801)
+// The "at" plane (the lens plane, RT:1790-1793) is emitted first: it depends on r only.
+// UNI: the media on both sides are uniform (Constant, or Vacuum with an ordinary wavelength on every lane of the
+// wave): F, B, n1 f and n1 n1 f + n2 n2 f come from the descriptor, computed on the host by the same operations.
+template <typename T, bool AX, bool UNI, typename EmitAt, class G>
+RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
+                       Ray<T>& after, G* g) {
+    const T f = s.f;
+    const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
+    // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
+    const Rcp<T> iden = make_rcp(axdot<AX>(r.dx, r.dy, r.dz, nx, ny, nz));
+    emit_at(to_plane<AX, AX>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
+                             g));   // RT:1790-1793
+    T Fx, Fy, Fz, Bx, By, Bz;
+    if constexpr (UNI) {
+        Fx = s.lF[0]; Fy = s.lF[1]; Fz = s.lF[2];
+        Bx = s.lB[0]; By = s.lB[1]; Bz = s.lB[2];
+    } else {
+        Fx = s.c[0] - s.nf[0] * n1; Fy = s.c[1] - s.nf[1] * n1; Fz = s.c[2] - s.nf[2] * n1;
+        Bx = s.c[0] + s.nf[0] * n2; By = s.c[1] + s.nf[1] * n2; Bz = s.c[2] + s.nf[2] * n2;
+    }
+    // axial and uniform: F = (+0, +0, Fz), so the front focal plane has the axial center form too
+    constexpr bool AXF = AX && UNI;
+    const Ray<T> rf = to_plane<AX, AXF>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
+    const T dn = axdot<AX>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
+    T spx, spy, spz;
+    if constexpr (AX) {
+        spx = tfma(-dn, T(0), rf.dx);                 // dx - dn * 0
+        spy = tfma(-dn, T(0), rf.dy);
+        spz = rf.dz - dn;                             // dz - dn * 1
+    } else {
+        spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
+    }
+    // |s1_perp| and |r1| (RT:1704-1728): a norm squared in range takes the combined test (norm2_fast), the
+    // rest the full tests -- bit-identical either way, NaN included
+    const T spv = spx * spx + spy * spy + spz * spz;
+    const T r1x = axsub<AXF>(rf.x, Fx), r1y = axsub<AXF>(rf.y, Fy), r1z = rf.z - Fz;
+    const T r1v = r1x * r1x + r1y * r1y + r1z * r1z;
+    T ux = r1x, uy = r1y, uz = r1z;
+    T r1n;
+#if defined(RTPB_FASTNORM)
+    if constexpr (sizeof(T) == 8 && !G::kDefer) {
+        if (__builtin_expect(norm2_fast(spv), 1)) {
+            const T spn = sqrt_core(spv);
+            if (spn > T(1e-12)) div3_norm<T, G, 1>(spx, spy, spz, make_rcp_in_range(spn), g);   // |s| <= norm
+        } else {
+            const T spn = sqrt(spv);                              // the compiler's full sequences
+            if (spn > T(1e-12)) {
+                spx = spx / spn; spy = spy / spn; spz = spz / spn;
+            }
+        }
+        if (__builtin_expect(norm2_fast(r1v), 1)) {
+            r1n = sqrt_core(r1v);
+            div3_norm<T, G, 1>(ux, uy, uz, make_rcp_in_range(r1n), g);   // r1n >= 2^-120 (or NaN: NaN out)
+        } else {
+            r1n = sqrt(r1v);
+            if (r1n != T(0)) {
+                ux = ux / r1n; uy = uy / r1n; uz = uz / r1n;
+            }
+        }
+    } else
+#endif
+    {
+        const T spn = tsqrt<T>(spv, g);
+        if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
+        r1n = tsqrt<T>(r1v, g);
+        if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
+    }
+    const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
+    Ray<T> o;
+    const T h = (UNI ? s.ln1f : n1 * f) * sin_t1;                  // (n1 f) sin_t1, RT:1755
+    o.x = h * spx + Bx;
+    o.y = h * spy + By;
+    o.z = h * spz + Bz;
+    // -r1n is a norm (bounded, see NUM_IN_RANGE); with 2^-80 <= |f| < 2^120 (host bit kLensQ1) so is q1 =
+    // -r1n / f: 2^-657 <= |q1| <= 2^592, or 0, inf, NaN
+    const T q1 = div1<T, G, true>(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
+    T sin_t2;
+    if (s.rcp_ok & 8) {
+        RTPB_NO_SPECULATE();
+        if (s.rcp_ok & kLensQ1) sin_t2 = div1<T, G, true>(q1, host_rcp(n2, s.rn2, true), g);
+        else sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
+    } else {
+        sin_t2 = q1 / n2;
+    }
+    const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
+    if constexpr (AX) {
+        o.dx = tfma(cos_t2, T(0), sin_t2 * ux);
+        o.dy = tfma(cos_t2, T(0), sin_t2 * uy);
+        o.dz = sin_t2 * uz + cos_t2;
+    } else {
+        o.dx = sin_t2 * ux + cos_t2 * nx;
+        o.dy = sin_t2 * uy + cos_t2 * ny;
+        o.dz = sin_t2 * uz + cos_t2 * nz;
+    }
+    o.wl = r.wl;
+    kill_if(tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a, o);
+    const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
+    // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
+    const T k = iwl.k;
+    o.ph = rf.ph - k * n1 * pw + k * (UNI ? s.lph : n1 * n1 * f + n2 * n2 * f);
+    after = to_plane<AX, AX>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
+                             static_cast<const Rcp<T>*>(nullptr), g);
+}
+
 // ------------------------------------------------------------------ one surface: (at, after)
 // Refracting surfaces RT:1160-1234, reflecting RT:1238-1303, PerfectLens RT:1601-1801.
 // One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
@@ -749,96 +895,14 @@ template <typename T, int KIND, bool AX = false, typename EmitAt, class G = Guar
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                           Ray<T>& after, G* g = nullptr) {
     if constexpr (KIND == PERFECT_LENS) {
-        const T f = s.f;
-        const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
-        // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
-        const Rcp<T> iden = make_rcp(axdot<AX>(r.dx, r.dy, r.dz, nx, ny, nz));
-        emit_at(to_plane<AX, AX>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
-                                 g));   // RT:1790-1793
-        // (host-side F, B and n^2 f for uniform media measured 3 % slower on C4: the merged values cost
-        // registers, profiles/r03/experiments/ab_lens_constants.log)
-        const T Fx = s.c[0] - s.nf[0] * n1, Fy = s.c[1] - s.nf[1] * n1, Fz = s.c[2] - s.nf[2] * n1;
-        const T Bx = s.c[0] + s.nf[0] * n2, By = s.c[1] + s.nf[1] * n2, Bz = s.c[2] + s.nf[2] * n2;
-        const Ray<T> rf = to_plane<AX, false>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
-        const T dn = axdot<AX>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
-        T spx, spy, spz;
-        if constexpr (AX) {
-            spx = tfma(-dn, T(0), rf.dx);                 // dx - dn * 0
-            spy = tfma(-dn, T(0), rf.dy);
-            spz = rf.dz - dn;                             // dz - dn * 1
-        } else {
-            spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
-        }
-        // |s1_perp| and |r1| (RT:1704-1728): a norm squared in range takes the combined test (norm2_fast), the
-        // rest the full tests -- bit-identical either way, NaN included
-        const T spv = spx * spx + spy * spy + spz * spz;
-        const T r1x = rf.x - Fx, r1y = rf.y - Fy, r1z = rf.z - Fz;
-        const T r1v = r1x * r1x + r1y * r1y + r1z * r1z;
-        T ux = r1x, uy = r1y, uz = r1z;
-        T r1n;
-#if defined(RTPB_FASTNORM)
-        if constexpr (sizeof(T) == 8 && !G::kDefer) {
-            if (__builtin_expect(norm2_fast(spv), 1)) {
-                const T spn = sqrt_core(spv);
-                if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp_in_range(spn), g);
-            } else {
-                const T spn = sqrt(spv);                              // the compiler's full sequences
-                if (spn > T(1e-12)) {
-                    spx = spx / spn; spy = spy / spn; spz = spz / spn;
-                }
-            }
-            if (__builtin_expect(norm2_fast(r1v), 1)) {
-                r1n = sqrt_core(r1v);
-                div3_norm(ux, uy, uz, make_rcp_in_range(r1n), g);     // r1n >= 2^-120 or NaN: != 0
-            } else {
-                r1n = sqrt(r1v);
-                if (r1n != T(0)) {
-                    ux = ux / r1n; uy = uy / r1n; uz = uz / r1n;
-                }
-            }
-        } else
-#endif
-        {
-            const T spn = tsqrt<T>(spv, g);
-            if (spn > T(1e-12)) div3_norm(spx, spy, spz, make_rcp(spn), g);
-            r1n = tsqrt<T>(r1v, g);
-            if (r1n != T(0)) div3_norm(ux, uy, uz, make_rcp(r1n), g);
-        }
-        const T sin_t1 = spx * rf.dx + spy * rf.dy + spz * rf.dz;
-        Ray<T> o;
-        const T h = n1 * f * sin_t1;
-        o.x = h * spx + Bx;
-        o.y = h * spy + By;
-        o.z = h * spz + Bz;
-        // -r1n is a norm (bounded, see NUM_IN_RANGE); with 2^-80 <= |f| < 2^120 (host bit kLensQ1) so is q1 =
-        // -r1n / f: 2^-657 <= |q1| <= 2^592, or 0, inf, NaN
-        const T q1 = div1<T, G, true>(-r1n, host_rcp(f, s.rf, (s.rcp_ok & 2) != 0), g);
-        T sin_t2;
-        if (s.rcp_ok & 8) {
+        // uniform media: the instantiation with the focal points and constants in scalar registers (a wave-uniform
+        // branch between two whole steps: merged values would cost vector registers on both paths)
+        if (s.rcp_ok & kLensUni) {
             RTPB_NO_SPECULATE();
-            if (s.rcp_ok & kLensQ1) sin_t2 = div1<T, G, true>(q1, host_rcp(n2, s.rn2, true), g);
-            else sin_t2 = div1(q1, host_rcp(n2, s.rn2, true), g);
+            lens_step<T, AX, true>(s, r, n1, n2, iwl, emit_at, after, g);
         } else {
-            sin_t2 = q1 / n2;
+            lens_step<T, AX, false>(s, r, n1, n2, iwl, emit_at, after, g);
         }
-        const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
-        if constexpr (AX) {
-            o.dx = tfma(cos_t2, T(0), sin_t2 * ux);
-            o.dy = tfma(cos_t2, T(0), sin_t2 * uy);
-            o.dz = sin_t2 * uz + cos_t2;
-        } else {
-            o.dx = sin_t2 * ux + cos_t2 * nx;
-            o.dy = sin_t2 * uy + cos_t2 * ny;
-            o.dz = sin_t2 * uz + cos_t2 * nz;
-        }
-        o.wl = r.wl;
-        kill_if(tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a, o);
-        const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
-        // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
-        const T k = iwl.k;
-        o.ph = rf.ph - k * n1 * pw + k * (n1 * n1 * f + n2 * n2 * f);
-        after = to_plane<AX, AX>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
-                                 static_cast<const Rcp<T>*>(nullptr), g);
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
@@ -851,7 +915,18 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
                 // kAxial spheres have a finite shell_hi: where the on-surface test passes (the only rays whose
                 // normal reaches a stored value) each |p - c| component is below sqrt(shell_hi) < 2^513, so the
                 // numerators need only the lower bound of the exact range (div3_norm's single min3 test)
-                div3_norm(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
+                // a finite nonzero radius in the shortcut range (host bits kRPos / kRNeg): no div_fixup -- the
+                // numerators of every row that survives the on-surface test are finite (above)
+                const Rcp<T> iR = host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0);
+                if (s.rcp_ok & kRPos) {
+                    RTPB_NO_SPECULATE();
+                    div3_norm<T, G, 1>(Nx, Ny, Nz, iR, g);
+                } else if (s.rcp_ok & kRNeg) {
+                    RTPB_NO_SPECULATE();
+                    div3_norm<T, G, -1>(Nx, Ny, Nz, iR, g);
+                } else {
+                    div3_norm(Nx, Ny, Nz, iR, g);
+                }
             } else {
                 div3(Nx, Ny, Nz, host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0), g);
             }
@@ -1065,6 +1140,7 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     d.rR = 1.0 / s.radius;                       // IEEE division: RN(1/R) (inf for R = 0)
     d.rf = 1.0 / s.focal_len;
     d.rcp_ok = (host_rcp_ok(s.radius) ? 1 : 0) | (host_rcp_ok(s.focal_len) ? 2 : 0);
+    if (host_rcp_ok(s.radius) && std::isfinite(s.radius) && s.radius != 0.0) d.rcp_ok |= s.radius > 0.0 ? kRPos : kRNeg;
     for (int j = 0; j < 3; ++j) d.nf[j] = s.normal[j] * s.focal_len;     // RT:1682-1687 `normal * focal_len`
     // kAxial: the exact +0 / 1 components the specialised steps rely on (bit patterns: -0 does not qualify)
     auto is_p0 = [](double v) { return host::bits(v) == 0; };
@@ -1099,6 +1175,19 @@ inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>
         // next to a Vacuum the values hold only for ordinary wavelengths: bits 4 / 8 moved to 16 / 32, which
         // the trace kernel turns into 4 / 8 when every ray of the wave has one
         d.rcp_ok |= (m1.kind == VACUUM || m2.kind == VACUUM) ? bits << 2 : bits;
+        if (d.kind == PERFECT_LENS && std::isfinite(n1) && std::isfinite(n2)) {
+            // the per-ray expressions of lens_step<..., false> with these n1, n2
+            for (int j = 0; j < 3; ++j) {
+                d.lF[j] = d.c[j] - d.nf[j] * n1;
+                d.lB[j] = d.c[j] + d.nf[j] * n2;
+            }
+            d.ln1f = n1 * d.f;
+            d.lph = n1 * n1 * d.f + n2 * n2 * d.f;
+            auto is_p0 = [](double v) { return host::bits(v) == 0; };
+            const bool on_axis = is_p0(d.lF[0]) && is_p0(d.lF[1]) && is_p0(d.lB[0]) && is_p0(d.lB[1]);
+            if (!(d.rcp_ok & kAxial) || on_axis)
+                d.rcp_ok |= (m1.kind == VACUUM || m2.kind == VACUUM) ? kLensUniVac : kLensUni;
+        }
     }
 }
 

@@ -129,6 +129,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     auto surface = [&](int s) -> DevSurface<T> {
         DevSurface<T> d = load_surface<T>(surf + s);
         if ((d.rcp_ok & 16) && vac_one) d.rcp_ok |= 4 | ((d.rcp_ok & 32) ? 8 : 0);
+        if ((d.rcp_ok & kLensUniVac) && vac_one) d.rcp_ok |= kLensUni;
         if constexpr (kIdx) {
             if (all_idx && !(d.rcp_ok & 4)) {
                 d.nr = lds_table[a.nkeys * (a.nsurf + 2 + s) + widx];

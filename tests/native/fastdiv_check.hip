@@ -14,7 +14,7 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kOut = 32;
+constexpr int kOut = 35;
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
@@ -24,7 +24,9 @@ constexpr int kOut = 32;
 //      [19..21] div3_norm((a, a2, a3), rcp(their norm)), [22..24] its GuardDefer form, [25] that flag,
 //      [26] sphere_root(B = a, root = tsqrt(|b|)), [27] signed_root(a, tsqrt(|b|)),
 //      [28..30] unit_or_zero(a, a2, a3) (the combined norm test, NaN components of the quotient replaced by 0),
-//      [31] the phase term |(a, a2, a3)| * 2 pi / b with the numerator's range implied (div1_as NUM_IN_RANGE)
+//      [31] the phase term |(a, a2, a3)| * 2 pi / b with the numerator's range implied (div1_as NUM_IN_RANGE),
+//      [32..34] div3_norm((a, a2, a3), host_rcp(b, yh)) in the axial sphere normal's form: without div_fixup
+//      (SIGN = +1 / -1) where b is finite, nonzero and in the divisor range, with it elsewhere
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -81,6 +83,14 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[30 * n + i] = fz;
     const double dist = tsqrt<double>(ai * ai + a2[i] * a2[i] + a3[i] * a3[i]);
     out[31 * n + i] = div1_as<double, GuardBranch, true>(dist * Const<double>::two_pi, bi, r);
+    double sx = ai, sy = a2[i], sz = a3[i];
+    const Rcp<double> hr = host_rcp(bi, yh[i], ok);
+    if (ok && bi > 0.0 && !isinf(bi)) div3_norm<double, GuardBranch, 1>(sx, sy, sz, hr);
+    else if (ok && bi < 0.0 && !isinf(bi)) div3_norm<double, GuardBranch, -1>(sx, sy, sz, hr);
+    else div3_norm(sx, sy, sz, hr);
+    out[32 * n + i] = sx;
+    out[33 * n + i] = sy;
+    out[34 * n + i] = sz;
 }
 
 }  // namespace

@@ -47,11 +47,18 @@ static int harness_trace(const rtpb_surface* surfaces, int32_t nsurf, const rtpb
         };
         put(0, r);
         const T wl0 = r.wl;
+        // the trace kernel's per-wave Vacuum test for a one-ray wave: an ordinary wavelength turns the Vacuum-side
+        // uniform-media bits into the plain ones (rtpb_trace_kernel.h, vac_one)
+        const T w2 = wl0 * wl0;
+        const bool vac_one = w2 != T(0) && w2 - w2 == T(0);
         T n_cur = material_n<T>(M[0], wl0, table.data());
         for (int s = 0; s < nsurf; ++s) {
             const T n_next = material_n<T>(M[s + 1], wl0, table.data());
             Ray<T> at, after;
-            propagate_surface<T>(S[s], r, n_cur, n_next, at, after);
+            DevSurface<T> d = S[s];
+            if ((d.rcp_ok & 16) && vac_one) d.rcp_ok |= 4 | ((d.rcp_ok & 32) ? 8 : 0);
+            if ((d.rcp_ok & kLensUniVac) && vac_one) d.rcp_ok |= kLensUni;
+            propagate_surface<T>(d, r, n_cur, n_next, at, after);
             put(2 * s + 1, at);
             put(2 * s + 2, after);
             r = after;

@@ -52,6 +52,13 @@ def _check(a, a2, a3, b, kill):
             exp = comp / nrm2
             _same(out[28 + k], np.where(np.isnan(exp), 0.0, exp))
         _same(out[31], nrm2 * (2 * np.pi) / b)     # a norm's range needs no numerator test (RT:297 order)
+        # the axial sphere normal (p - c) / R: no div_fixup for a finite nonzero R in the divisor range; its
+        # numerators are finite and at most 2^513 wherever the row survives the on-surface test
+        mb = np.abs(b)
+        in_b = (mb >= 2.0 ** -120) & (mb < 2.0 ** 120)
+        for k, comp in enumerate((a, a2, a3)):
+            sel = in_b & np.isfinite(comp) & (np.abs(comp) <= 2.0 ** 513)
+            _same(out[32 + k][sel], (comp / b)[sel])
         # GuardDefer: no fallback branch; where the flag is clear the value is the exact one, and the
         # flag is set only where an operand left the shortcut's exact range (the flagged rays are re-traced)
         for val, flag, exp in ((out[9], out[10], a / b), (out[11], out[14], a / b), (out[12], out[14], a2 / b),

@@ -6,6 +6,7 @@ switches (RTPB_EXP_NO_COMPUTE, XCD_REMAP, PERSIST, ...) are profiles/r02/experim
 which applies to the round-2 sources (commit 7b1cac3).
 
     python tools/exp_build.py --out ray_trace_pb_amd/exp_x.so --patch my.patch -DMY_SWITCH
+    python tools/exp_build.py --out ray_trace_pb_amd/exp_base.so --rev HEAD     # the committed sources (A/B base)
 """
 import argparse
 import os
@@ -19,10 +20,16 @@ sys.path.insert(0, ROOT)
 from ray_trace_pb_amd import _build  # noqa: E402
 
 
-def build(out, flags=(), patches=()):
+def build(out, flags=(), patches=(), rev=None):
     with tempfile.TemporaryDirectory() as tmp:
-        shutil.copytree(_build.CSRC, os.path.join(tmp, "ray_trace_pb_amd", "csrc"),
-                        ignore=shutil.ignore_patterns("_obj"))
+        if rev:
+            # the kernel sources (and include/) of a git revision
+            arch = subprocess.run(["git", "-C", ROOT, "archive", rev, "ray_trace_pb_amd/csrc", "include"],
+                                  check=True, capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", tmp], input=arch, check=True)
+        else:
+            shutil.copytree(_build.CSRC, os.path.join(tmp, "ray_trace_pb_amd", "csrc"),
+                            ignore=shutil.ignore_patterns("_obj"))
         for p in patches:
             subprocess.run(["patch", "-p1", "-s", "-d", tmp, "-i", os.path.abspath(p)], check=True)
         return _build.build(force=True, verbose=False, extra_flags=list(flags), out=os.path.abspath(out),
@@ -33,8 +40,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--patch", action="append", default=[])
+    ap.add_argument("--rev", default=None, help="build the csrc of this git revision instead of the working tree")
     args, flags = ap.parse_known_args()
-    print(build(args.out, flags, args.patch))
+    print(build(args.out, flags, args.patch, args.rev))
 
 
 if __name__ == "__main__":

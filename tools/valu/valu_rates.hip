@@ -16,9 +16,9 @@
 template <int OP>
 __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned long long* cyc, double* sink) {
     double a[8], b[8];
-    int ia[8];
+    int ia[8], ib[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { a[k] = seed + threadIdx.x * 1e-3 + k; b[k] = 1.0 + k * 1e-6; ia[k] = threadIdx.x + k; }
+    for (int k = 0; k < 8; ++k) { a[k] = seed + threadIdx.x * 1e-3 + k; b[k] = 1.0 + k * 1e-6; ia[k] = threadIdx.x + k; ib[k] = 3 * k + 1; }
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; ++i) {
 #define FMA(k) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(a[k]) : "v"(b[k]));
@@ -30,12 +30,12 @@ __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned lo
 #define FREXP(k) asm volatile("v_frexp_exp_i32_f64 %0, %1" : "=v"(ia[k]) : "v"(a[k]));
 #define CLASS(k) asm volatile("v_cmp_class_f64 vcc, %0, %1" : : "v"(a[k]), "v"(ia[k]) : "vcc");
 #define CMPF(k) asm volatile("v_cmp_lt_f64 vcc, %0, %1" : : "v"(a[k]), "v"(b[k]) : "vcc");
-#define CMPU(k) asm volatile("v_cmp_lt_u32 vcc, %0, %1" : : "v"(ia[k]), "v"(ia[(k + 1) & 7]) : "vcc");
-#define ADDU(k) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ia[k]) : "v"(ia[(k + 1) & 7]));
-#define CND(k) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(ia[k]) : "v"(ia[(k + 1) & 7]) : "vcc");
+#define CMPU(k) asm volatile("v_cmp_lt_u32 vcc, %0, %1" : : "v"(ia[k]), "v"(ib[k]) : "vcc");
+#define ADDU(k) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ia[k]) : "v"(ib[k]));
+#define CND(k) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(ia[k]) : "v"(ib[k]) : "vcc");
 #define MOV64(k) asm volatile("v_mov_b64 %0, %1" : "=v"(a[k]) : "v"(b[k]));
-#define MOV32(k) asm volatile("v_mov_b32 %0, %1" : "=v"(ia[k]) : "v"(ia[(k + 1) & 7]));
-#define MIN3(k) asm volatile("v_min3_i32 %0, %0, %1, %1" : "+v"(ia[k]) : "v"(ia[(k + 1) & 7]));
+#define MOV32(k) asm volatile("v_mov_b32 %0, %1" : "=v"(ia[k]) : "v"(ib[k]));
+#define MIN3(k) asm volatile("v_min3_i32 %0, %0, %1, %1" : "+v"(ia[k]) : "v"(ib[k]));
 #define MINF(k) asm volatile("v_min_f64 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
 #define LDEXP(k) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(a[k]) : "v"(ia[k]));
 #define FMAC(k) asm volatile("v_fmac_f64 %0, %1, %1" : "+v"(a[k]) : "v"(b[k]));
@@ -103,12 +103,14 @@ int main(int argc, char** argv) {
     const int iters = argc > 1 ? std::atoi(argv[1]) : 20000;
     hipDeviceProp_t p; CHECK(hipGetDeviceProperties(&p, 0));
     const int cus = p.multiProcessorCount;
-    std::printf("%s, %d CUs; 4 waves per SIMD, 8 independent chains per wave; cycles = s_memtime over the loop / "
-                "(instructions per wave x waves per SIMD)\n", p.gcnArchName, cus);
-    const int W = 4;
-    run<0>(iters, cus, W); run<17>(iters, cus, W); run<1>(iters, cus, W); run<2>(iters, cus, W); run<3>(iters, cus, W);
-    run<4>(iters, cus, W); run<5>(iters, cus, W); run<6>(iters, cus, W); run<7>(iters, cus, W); run<8>(iters, cus, W);
-    run<9>(iters, cus, W); run<10>(iters, cus, W); run<11>(iters, cus, W); run<12>(iters, cus, W); run<13>(iters, cus, W);
-    run<14>(iters, cus, W); run<15>(iters, cus, W); run<16>(iters, cus, W); run<18>(iters, cus, W); run<19>(iters, cus, W);
+    std::printf("%s, %d CUs; W waves per SIMD (one 4-wave block per CU per W), 8 independent chains per wave; cycles "
+                "= median s_memtime over a wave's loop / (its instructions x W)\n", p.gcnArchName, cus);
+    for (int W : {1, 2}) {
+        std::printf("-- W = %d\n", W);
+        run<0>(iters, cus, W); run<17>(iters, cus, W); run<1>(iters, cus, W); run<2>(iters, cus, W); run<3>(iters, cus, W);
+        run<4>(iters, cus, W); run<5>(iters, cus, W); run<6>(iters, cus, W); run<7>(iters, cus, W); run<8>(iters, cus, W);
+        run<9>(iters, cus, W); run<10>(iters, cus, W); run<11>(iters, cus, W); run<12>(iters, cus, W); run<13>(iters, cus, W);
+        run<14>(iters, cus, W); run<15>(iters, cus, W); run<16>(iters, cus, W); run<18>(iters, cus, W); run<19>(iters, cus, W);
+    }
     return 0;
 }
