@@ -131,11 +131,12 @@ __device__ __forceinline__ double stored(double v) { return static_cast<double>(
 #endif
 constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per block)
 
-// Occupancy: held to >= 7 waves per SIMD (<= 72 VGPRs; the compiler spills 6-8 values to scratch outside
-// the surface loop) -- 2.4 % faster than its natural 83 VGPRs / 5 waves on the full C5 sweep, 6 and 8 waves
-// in between (experiments/ab_sweep_wpe*.log, bit-identical).  RTPB_SWEEP_WPE overrides it (A/B builds).
+// Occupancy: held to >= 6 waves per SIMD (<= 80 VGPRs).  Round 3 measured 7 best (2.4 % faster than the natural
+// 83 VGPRs / 5 waves, experiments/ab_sweep_wpe*.log); with round 4's lens instantiation, fixup-free quotients and
+// x x + y y carry the sweep runs 0.379 s at 6, 0.384 s at 7, 0.401 s at 8 (profiles/r04/e/, one process,
+// bit-identical).  RTPB_SWEEP_WPE overrides it (A/B builds).
 #ifndef RTPB_SWEEP_WPE
-#define RTPB_SWEEP_WPE 7
+#define RTPB_SWEEP_WPE 6
 #endif
 #define RTPB_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(RTPB_SWEEP_WPE, 8)))
 template <typename TS, int FEAT>
@@ -178,12 +179,21 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     // surface step, so the rays' registers carry from surface to surface without the copies a per-surface
     // join of the kind branches needs (the ODT path of C5: 12 axial spheres, a lens, a flat = 3 runs)
     auto code_of = [&](int k) { return surface_code<double>((surf + k)->kind, (surf + k)->rcp_ok); };
+    // the statistics read only the final positions: the steps run with kPosOnly semantics (no TIR fill of the
+    // position -- the next surface's intersection makes it NaN, and the final plane gets the rule below), and a run
+    // of axial spheres carries x x + y y of each intersection point into the next sphere's quadratic
+    double rxy[kSweepRays];
     int s = 0;
     while (s < a.nsurf) {
         const int code = code_of(s);
         dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
             constexpr int K = decltype(kind)::value;
             constexpr bool A = decltype(ax)::value;
+            constexpr bool kCarry = K == SPHERE && A;
+            if constexpr (kCarry) {
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q) rxy[q] = r[q].x * r[q].x + r[q].y * r[q].y;
+            }
             do {
                 const double n_next = mat_n(s + 1);
                 DevSurface<double> sd = load_surface<double>(surf + s);
@@ -197,7 +207,8 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
                 Ray<double> o[kSweepRays];
 #pragma unroll
                 for (int q = 0; q < kSweepRays; ++q)
-                    surface_step<double, K, A>(sd, r[q], n_cur, n_next, iwl, none, o[q]);
+                    surface_step<double, K, A, kPosOnly>(sd, r[q], n_cur, n_next, iwl, none, o[q],
+                                                         static_cast<GuardBranch*>(nullptr), kCarry ? &rxy[q] : nullptr);
 #pragma unroll
                 for (int q = 0; q < kSweepRays; ++q) r[q] = o[q];
                 n_cur = n_next;
@@ -207,7 +218,9 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     }
     auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
         double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
-        if (ok) {
+        // the reference's position rule of the last surface (RT:1221 / RT:1289; a PerfectLens's after-plane
+        // propagation gives a NaN position for a NaN direction by itself): NaN direction -> no spot point
+        if (ok && !is_nan(r.dx)) {
             const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
             if (x - x == 0.0 && y - y == 0.0) {
                 v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;

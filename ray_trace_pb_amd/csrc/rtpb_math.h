@@ -175,6 +175,22 @@ RTPB_HD T tsqrt(T v, G* g = nullptr) {
     }
 }
 
+// sqrt(1 - m m) (Snell's tangential root RT:1217, PerfectLens cos_t2 RT:1763): the argument w = RN(1 - RN(m m)) is
+// NaN, negative, +0 or at least 2^-53 -- RN(m m) < 1 is a multiple of 2^-53 where it is at least 1/2 (so 1 - it is
+// exact), and w > 1/2 elsewhere -- so +0 (|m| = 1) is the only argument the square-root core cannot take: one
+// compare instead of tsqrt's class and range tests
+template <typename T, class G = GuardBranch>
+RTPB_HD T tsqrt_1m(T w, G* g = nullptr) {
+#if defined(RTPB_FASTSQRT)
+    if constexpr (sizeof(T) == 8 && !G::kDefer) {
+        T s = sqrt_core(w);
+        if (__builtin_expect(w == T(0), 0)) s = sqrt(w);
+        return s;
+    }
+#endif
+    return tsqrt<T>(w, g);
+}
+
 // numpy.abs: |v| with +0 for -0 -- the sign-bit clear (one VALU, or a free operand modifier in a compare)
 template <typename T> RTPB_HD T tabs(T v) { return std::fabs(v); }
 
@@ -605,11 +621,14 @@ RTPB_HD T sphere_root(T B, T root) {
     return t;
 }
 
+// rxy (AX only): x x + y y of the ray's position, as on_sphere computed it at the previous axial surface (the
+// same expression for a center on the axis) -- or nullptr
 template <bool AX = false, typename T, class G = GuardBranch>
-RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr) {
+RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr,
+                          const T* rxy = nullptr) {
     const T ox = axsub<AX>(r.x, s.c[0]), oy = axsub<AX>(r.y, s.c[1]), oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
-    const T C = ox * ox + oy * oy + oz * oz - s.R2;
+    const T C = ((AX && rxy) ? *rxy : ox * ox + oy * oy) + oz * oz - s.R2;
     const T t = sphere_root(B, tsqrt<T>(B * B - T(4) * C, g));
     Ray<T> o;
     o.x = r.x + r.dx * t;
@@ -708,12 +727,15 @@ RTPB_HD T signed_root(T v, T root) {
 // Snell refraction of the intersected ray (RT:1197-1221)
 // ratio: n1 / n2, computed by the caller (per lane, or once on the host for uniform media)
 // AX: N == (+0, +0, 1) (axdot)
-template <bool AX = false, typename T, class G = GuardBranch>
+// TIR_FILL = false (the spot sweep's final-position semantics, kPosOnly): the position is left as it is where the
+// direction is NaN -- the next surface's intersection turns it into NaN, and the sweep applies the rule to the
+// final plane itself
+template <bool AX = false, bool TIR_FILL = true, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
     T cx, cy, cz;
     tangent_basis<AX>(ri, Nx, Ny, Nz, cx, cy, cz, g);
     const T mag = ratio * (cx * ri.dx + cy * ri.dy + cz * ri.dz);
-    const T tang = signed_root(axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz), tsqrt<T>(T(1) - mag * mag, g));
+    const T tang = signed_root(axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz), tsqrt_1m<T>(T(1) - mag * mag, g));
     Ray<T> o;
     if constexpr (AX) {
         o.dx = tfma(tang, T(0), mag * cx);
@@ -727,8 +749,10 @@ RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr
     o.x = ri.x; o.y = ri.y; o.z = ri.z;
     o.ph = ri.ph;
     o.wl = ri.wl;
-    if (__builtin_expect(is_nan(o.dx), 0)) {       // TIR (and dead rows): position NaN only (RT:1221)
-        o.x = qnan<T>(); o.y = qnan<T>(); o.z = qnan<T>();
+    if constexpr (TIR_FILL) {
+        if (__builtin_expect(is_nan(o.dx), 0)) {   // TIR (and dead rows): position NaN only (RT:1221)
+            o.x = qnan<T>(); o.y = qnan<T>(); o.z = qnan<T>();
+        }
     }
     return o;
 }
@@ -766,9 +790,10 @@ RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
 // makes p finite; then a = p.z up to a zero sign, q = (p.x -+ 0, p.y -+ 0, +-0), and the aperture sum
 // (qx qx + qy qy) + qz qz is exactly p.x p.x + p.y p.y -- the first partial sum of d2.
 template <bool AX = false, typename T>
-RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s) {
+RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s, T* rxy_out = nullptr) {
     const T rx = axsub<AX>(p.x, s.c[0]), ry = axsub<AX>(p.y, s.c[1]), rz = p.z - s.c[2];
     const T rxy = rx * rx + ry * ry;
+    if (rxy_out) *rxy_out = rxy;
     const T d2 = rxy + rz * rz;
     const bool on = d2 >= s.shell_lo && d2 <= s.shell_hi;                      // |norm(p - c) - |R|| < tol
     if constexpr (AX) {
@@ -865,7 +890,7 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     } else {
         sin_t2 = q1 / n2;
     }
-    const T cos_t2 = tsqrt<T>(T(1) - sin_t2 * sin_t2, g);
+    const T cos_t2 = tsqrt_1m<T>(T(1) - sin_t2 * sin_t2, g);
     if constexpr (AX) {
         o.dx = tfma(cos_t2, T(0), sin_t2 * ux);
         o.dy = tfma(cos_t2, T(0), sin_t2 * uy);
@@ -891,9 +916,14 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
 // AX: the surface has kAxial geometry (not for PLANE_MIRROR).
-template <typename T, int KIND, bool AX = false, typename EmitAt, class G = GuardBranch>
+// MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell).
+// rxy (kAxial spheres in kPosOnly runs): in: x x + y y of r (on_sphere's value at the previous axial surface); out:
+// the same of the intersection point, for the next one.
+constexpr int kPosOnly = 1;
+template <typename T, int KIND, bool AX = false, int MODE = 0, typename EmitAt, class G = GuardBranch>
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
-                          Ray<T>& after, G* g = nullptr) {
+                          Ray<T>& after, G* g = nullptr, T* rxy = nullptr) {
+    constexpr bool kTirFill = (MODE & kPosOnly) == 0;
     if constexpr (KIND == PERFECT_LENS) {
         // uniform media: the instantiation with the focal points and constants in scalar registers (a wave-uniform
         // branch between two whole steps: merged values would cost vector registers on both paths)
@@ -907,7 +937,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         T Nx, Ny, Nz;
         Ray<T> ri;
         if constexpr (KIND == SPHERE) {
-            ri = sphere_hit<AX>(r, s, n1, iwl, g);
+            ri = sphere_hit<AX>(r, s, n1, iwl, g, static_cast<const T*>(rxy));
             Nx = axsub<AX>(ri.x, s.c[0]);                                  // (p - c) / R, RT:1476
             Ny = axsub<AX>(ri.y, s.c[1]);
             Nz = ri.z - s.c[2];
@@ -950,8 +980,10 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             } else {
                 ratio = n1 / n2;
             }
-            after = snell<AX && KIND == FLAT>(ri, Nx, Ny, Nz, ratio, g);
-            const bool ok = (KIND == SPHERE) ? on_sphere<AX>(ri, s) : on_flat<AX>(ri, s);
+            after = snell<AX && KIND == FLAT, kTirFill>(ri, Nx, Ny, Nz, ratio, g);
+            bool ok;
+            if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy);
+            else ok = on_flat<AX>(ri, s);
             kill_if(!ok, after);
         }
     }
