@@ -17,8 +17,10 @@ template <int OP>
 __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned long long* cyc, double* sink) {
     double a[8], b[8];
     int ia[8], ib[8];
+    unsigned long long sm[8];
+    float fa[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { a[k] = seed + threadIdx.x * 1e-3 + k; b[k] = 1.0 + k * 1e-6; ia[k] = threadIdx.x + k; ib[k] = 3 * k + 1; }
+    for (int k = 0; k < 8; ++k) { a[k] = seed + threadIdx.x * 1e-3 + k; b[k] = 1.0 + k * 1e-6; ia[k] = threadIdx.x + k; ib[k] = 3 * k + 1; sm[k] = 0x5555ull << k; fa[k] = 0.f; }
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; ++i) {
 #define FMA(k) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(a[k]) : "v"(b[k]));
@@ -28,16 +30,17 @@ __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned lo
 #define RSQ(k) asm volatile("v_rsq_f64 %0, %0" : "+v"(a[k]));
 #define FIX(k) asm volatile("v_div_fixup_f64 %0, %0, %1, %1" : "+v"(a[k]) : "v"(b[k]));
 #define FREXP(k) asm volatile("v_frexp_exp_i32_f64 %0, %1" : "=v"(ia[k]) : "v"(a[k]));
-#define CLASS(k) asm volatile("v_cmp_class_f64 vcc, %0, %1" : : "v"(a[k]), "v"(ia[k]) : "vcc");
-#define CMPF(k) asm volatile("v_cmp_lt_f64 vcc, %0, %1" : : "v"(a[k]), "v"(b[k]) : "vcc");
-#define CMPU(k) asm volatile("v_cmp_lt_u32 vcc, %0, %1" : : "v"(ia[k]), "v"(ib[k]) : "vcc");
+#define CLASS(k) asm volatile("v_cmp_class_f64_e64 %0, %1, %2" : "=s"(sm[k]) : "v"(a[k]), "v"(ia[k]));
+#define CMPF(k) asm volatile("v_cmp_lt_f64_e64 %0, %1, %2" : "=s"(sm[k]) : "v"(a[k]), "v"(b[k]));
+#define CMPU(k) asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(sm[k]) : "v"(ia[k]), "v"(ib[k]));
 #define ADDU(k) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ia[k]) : "v"(ib[k]));
-#define CND(k) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(ia[k]) : "v"(ib[k]) : "vcc");
+#define CND(k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(ia[k]) : "v"(ib[k]), "s"(sm[k]));
 #define MOV64(k) asm volatile("v_mov_b64 %0, %1" : "=v"(a[k]) : "v"(b[k]));
 #define MOV32(k) asm volatile("v_mov_b32 %0, %1" : "=v"(ia[k]) : "v"(ib[k]));
 #define MIN3(k) asm volatile("v_min3_i32 %0, %0, %1, %1" : "+v"(ia[k]) : "v"(ib[k]));
 #define MINF(k) asm volatile("v_min_f64 %0, %0, %1" : "+v"(a[k]) : "v"(b[k]));
 #define LDEXP(k) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(a[k]) : "v"(ia[k]));
+#define CVT(k) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(fa[k]) : "v"(a[k]));
 #define FMAC(k) asm volatile("v_fmac_f64 %0, %1, %1" : "+v"(a[k]) : "v"(b[k]));
         if constexpr (OP == 0) { REP8(FMA) }
         else if constexpr (OP == 1) { REP8(ADD) }
@@ -59,11 +62,12 @@ __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned lo
         else if constexpr (OP == 17) { REP8(FMAC) }
         else if constexpr (OP == 18) { REP8(FMA) REP8(ADDU) }        // a 2:1 mix... (f64 then int)
         else if constexpr (OP == 19) { REP8(FMA) REP8(RCP) }         // transcendental beside f64 FMAs
+        else if constexpr (OP == 20) { REP8(CVT) }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     double s = 0; int si = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { s += a[k]; si += ia[k]; }
+    for (int k = 0; k < 8; ++k) { s += a[k] + fa[k]; si += ia[k] + int(sm[k] & 1); }
     sink[blockIdx.x * 256 + threadIdx.x] = s + si;
     if (threadIdx.x % 64 == 0) cyc[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;
 }
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(256) void bench(int iters, double seed, unsigned lo
 static const char* kNames[] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_rcp_f64", "v_rsq_f64", "v_div_fixup_f64",
                                "v_frexp_exp_i32_f64", "v_cmp_class_f64", "v_cmp_lt_f64", "v_cmp_lt_u32", "v_add_u32",
                                "v_cndmask_b32", "v_mov_b64", "v_mov_b32", "v_min3_i32", "v_min_f64", "v_ldexp_f64",
-                               "v_fmac_f64", "8 v_fma_f64 + 8 v_add_u32", "8 v_fma_f64 + 8 v_rcp_f64"};
+                               "v_fmac_f64", "8 v_fma_f64 + 8 v_add_u32", "8 v_fma_f64 + 8 v_rcp_f64", "v_cvt_f32_f64"};
 
 template <int OP>
 void run(int iters, int cus, int waves_per_simd) {
@@ -105,12 +109,13 @@ int main(int argc, char** argv) {
     const int cus = p.multiProcessorCount;
     std::printf("%s, %d CUs; W waves per SIMD (one 4-wave block per CU per W), 8 independent chains per wave; cycles "
                 "= median s_memtime over a wave's loop / (its instructions x W)\n", p.gcnArchName, cus);
-    for (int W : {1, 2}) {
+    for (int W : {1, 2, 4}) {
         std::printf("-- W = %d\n", W);
         run<0>(iters, cus, W); run<17>(iters, cus, W); run<1>(iters, cus, W); run<2>(iters, cus, W); run<3>(iters, cus, W);
         run<4>(iters, cus, W); run<5>(iters, cus, W); run<6>(iters, cus, W); run<7>(iters, cus, W); run<8>(iters, cus, W);
         run<9>(iters, cus, W); run<10>(iters, cus, W); run<11>(iters, cus, W); run<12>(iters, cus, W); run<13>(iters, cus, W);
         run<14>(iters, cus, W); run<15>(iters, cus, W); run<16>(iters, cus, W); run<18>(iters, cus, W); run<19>(iters, cus, W);
+        run<20>(iters, cus, W);
     }
     return 0;
 }
