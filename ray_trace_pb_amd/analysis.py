@@ -75,7 +75,10 @@ def spot_sweep(system, initial_material, final_material, field_points, wavelengt
     G = field_points.shape[0] * wavelengths.size
     per = n_thetas * nphis
     mats = [initial_material] + list(system.materials) + [final_material]
-    low = E.lower(system.surfaces, mats, lambda: np.unique(wavelengths), code)
+    # tabulated materials are lowered at the wavelengths the kernels see: the group's wavelength rounded to the
+    # storage type (a float32 sweep's rays carry float32 wavelengths, and the table lookup matches exactly)
+    keys = wavelengths if tdt == torch.float64 else wavelengths.astype(np.float32).astype(np.float64)
+    low = E.lower(system.surfaces, mats, lambda: np.unique(keys), code)
     S = len(system.surfaces)
     if fused:
         devs = [dev] if devices is None else [torch.device("cuda", int(d)) for d in devices]

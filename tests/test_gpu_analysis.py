@@ -91,17 +91,29 @@ def test_spot_sweep_matches_oracle_c5_small():
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
-@pytest.mark.parametrize("case", ["c5", "c2"])
+@pytest.mark.parametrize("case", ["c5", "c2", "tir", "tir_last", "stress"])
 def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     """One-kernel sweep (generate + trace + reduce) == fan kernel + trace(planes='final') + spot stats,
     bit for bit, for a lens system (C5) and a lens-free one (C2), in both storage types; several
-    batches, ragged group size (not a multiple of 256)."""
+    batches, ragged group size (not a multiple of 256).  The sweep runs the surface steps with final-position
+    semantics (no per-surface TIR position fill, the final plane's rule applied at the end) and carries
+    x x + y y between axial spheres: the TIR prism (total internal reflection mid-path and, in 'tir_last', at
+    the final surface), and the stress system (every surface kind, a mirror, misses, aperture and NA kills,
+    tabulated and polynomial materials) check those against the full-semantics trace kernel."""
     if case == "c5":
         system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
         fields, wls, theta = systems.c5_field_points(2), [0.405, 0.532, 0.785], 0.5 * np.pi / 180
-    else:
+    elif case == "c2":
         system, m0, m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
         fields, wls, theta = [[0.0, 0.0, -5.0], [1.0, -2.0, -5.0]], list(systems.C2_WAVELENGTHS), 0.05
+    elif case in ("tir", "tir_last"):
+        system, _, m0, m1 = systems.tir_prism(rt, mat)
+        if case == "tir_last":
+            system = rt.System(system.surfaces[:2], system.materials[:1])
+        fields, wls, theta = [[0.0, 0.0, -5.0], [2.0, -1.0, -5.0]], [0.45, 0.55, 0.7], 0.5
+    else:
+        system, m0, m1 = systems.stress_system(rt, mat), mat.Vacuum(), mat.Vacuum()
+        fields, wls, theta = [[0.0, 0.0, -10.0], [3.0, -2.0, -10.0], [-1.5, 2.5, -10.0]], [0.5, 0.6328], 0.3
     args = (system, m0, m1, fields, wls, theta, 301, 77)
     fu, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=4, fused=True)
     un, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=5, fused=False)
@@ -109,6 +121,8 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     for k in fu:
         assert same_bits(fu[k], un[k]), k
     assert fu["count"].min() > 0
+    if case != "c5" and case != "c2":
+        assert (fu["count"] < 301 * 77).any()            # some rays of the bundle are lost on the way
 
 
 def test_dist_pt2plane_bitwise_vs_reference():
