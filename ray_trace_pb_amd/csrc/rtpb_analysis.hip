@@ -123,9 +123,9 @@ template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
 
 // kSweepRays rays per lane: block b covers tiles kSweepRays*b ... of its group; the rays go through each
-// surface in one straight-line region (propagate_surface_multi) so independent dependency chains
-// interleave (two: -6 % vs one ray per lane); each tile is reduced separately, with the same tree as
-// spot_partial_kernel.
+// surface in one straight-line region (one surface_step instantiation per ray, inside one run of equal surface
+// codes) so independent dependency chains interleave (two: -6 % vs one ray per lane); each tile is reduced
+// separately, with the same tree as spot_partial_kernel.
 #ifndef RTPB_SWEEP_RPL
 #define RTPB_SWEEP_RPL 2
 #endif

@@ -1059,43 +1059,6 @@ RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n
     });
 }
 
-// Two independent rays through the same surface: one kind dispatch, both bodies in one straight-line
-// region so the scheduler can interleave their dependency chains.
-template <typename T, bool WITH_LENS = true, class G = GuardBranch>
-RTPB_HD void propagate_surface_pair(const DevSurface<T>& s, const Ray<T>& ra, const Ray<T>& rb, T n1, T n2,
-                                    const Rcp<T>& iwl_a, const Rcp<T>& iwl_b, Ray<T>& after_a, Ray<T>& after_b,
-                                    G* g = nullptr) {
-    auto none = [](const Ray<T>&) {};
-    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
-        constexpr int K = decltype(kind)::value;
-        constexpr bool A = decltype(ax)::value;
-        surface_step<T, K, A>(s, ra, n1, n2, iwl_a, none, after_a, g);
-        surface_step<T, K, A>(s, rb, n1, n2, iwl_b, none, after_b, g);
-    });
-}
-
-// R independent rays through the same surface, in place (R = 2 is propagate_surface_pair).
-template <typename T, bool WITH_LENS, int R, class G = GuardBranch>
-RTPB_HD void propagate_surface_multi(const DevSurface<T>& s, Ray<T> (&r)[R], T n1, T n2, const Rcp<T>& iwl,
-                                     G* g = nullptr) {
-    if constexpr (R == 2) {
-        Ray<T> a, b;
-        propagate_surface_pair<T, WITH_LENS>(s, r[0], r[1], n1, n2, iwl, iwl, a, b, g);
-        r[0] = a;
-        r[1] = b;
-    } else {
-        auto none = [](const Ray<T>&) {};
-        Ray<T> o[R];
-        dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                surface_step<T, decltype(kind)::value, decltype(ax)::value>(s, r[q], n1, n2, iwl, none, o[q], g);
-        });
-#pragma unroll
-        for (int q = 0; q < R; ++q) r[q] = o[q];
-    }
-}
-
 template <typename T, bool WITH_LENS = true>
 RTPB_HD void propagate_surface(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, Ray<T>& at, Ray<T>& after) {
     propagate_surface_emit<T, WITH_LENS>(s, r, n1, n2, make_wl_rcp(r.wl), [&](const Ray<T>& v) { at = v; }, after);
