@@ -688,6 +688,37 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
     }
 }
 
+// A nearly unit vector over its norm, NaN components replaced by 0: nc = N x nb (RT:1207-1209), with N a unit normal
+// and nb a unit tangent, has |nc|^2 = |N|^2 |nb|^2 - (N . nb)^2 within a few ulps of 1 on every live row away from
+// normal incidence.  For |v - 1| <= 2^-31 the square root and the reciprocal the quotients need are read off the
+// bit pattern of v: with d = bits(v) - bits(1) (there the low word of v as a signed 32-bit integer) and m = d >> 1,
+//   RN(sqrt(v)) = bits(1) + m,   RN(1 / RN(sqrt(v))) = bits(1) - 2m (m >= 0) or bits(1) + ceil(-m / 2) (m < 0)
+// as bit patterns (sqrt(1 + k 2^-52) = 1 + k 2^-53 - k^2 2^-107 ..., just below a midpoint for odd k; below 1 the
+// steps are 2^-53; checked exhaustively for |d| <= 2^22 against NumPy in tests/test_math_harness.py), and
+// Markstein's correction with the correctly rounded reciprocal yields correctly rounded quotients -- the bits of
+// the compiler's sequences, which also round correctly.  ~11 integer operations replace two transcendental-seeded
+// sequences (rsq + 9, rcp + 4); other v take unit_or_zero.
+template <typename T, class G = GuardBranch>
+RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
+#if defined(RTPB_FASTNORM)
+    if constexpr (sizeof(T) == 8 && !G::kDefer) {
+        const T v = x * x + y * y + z * z;
+        if (__builtin_expect(tabs<T>(v - T(1)) <= T(0x1p-31), 1)) {      // v - 1 is exact (Sterbenz); NaN fails
+            const int32_t d = __double2loint(v);
+            const int32_t m = d >> 1;
+            const int32_t neg = m >> 31;                                // -1 where m < 0
+            // m >= 0 ? -2m : ceil(-m / 2), as a bit select (no branch)
+            const int32_t t = (neg & ((1 - m) >> 1)) | (~neg & -(m << 1));
+            const double s = __hiloint2double(0x3FF00000 + neg, m);
+            const double yr = __hiloint2double(0x3FF00000 + (t >> 31), t);
+            div3_norm<T, G, 1>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // components at most ~1: no fixup
+            return;
+        }
+    }
+#endif
+    unit_or_zero(x, y, z, g);
+}
+
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
 // AX: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot)
 template <bool AX = false, typename T, class G = GuardBranch>
@@ -712,7 +743,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         cy = Nz * bx - Nx * bz;
         cz = Nx * by - Ny * bx;
     }
-    unit_or_zero(cx, cy, cz, g);
+    unit_near1_or_zero(cx, cy, cz, g);
 }
 
 // np.sign(v) * root for root >= +0 or NaN (RT:1217; 1 - m^2 is never -0): for v < 0 or v > 0 the product is

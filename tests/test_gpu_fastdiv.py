@@ -51,6 +51,7 @@ def _check(a, a2, a3, b, kill):
         for k, comp in enumerate((a, a2, a3)):
             exp = comp / nrm2
             _same(out[28 + k], np.where(np.isnan(exp), 0.0, exp))
+            _same(out[35 + k], np.where(np.isnan(exp), 0.0, exp))    # unit_near1_or_zero: the same values
         _same(out[31], nrm2 * (2 * np.pi) / b)     # a norm's range needs no numerator test (RT:297 order)
         # the axial sphere normal (p - c) / R: no div_fixup for a finite nonzero R in the divisor range; its
         # numerators are finite and at most 2^513 wherever the row survives the on-surface test
@@ -165,3 +166,29 @@ def test_fused_norm_test_range_edges():
     a2[::89] = np.nan
     kill = np.zeros(n, dtype=np.uint8)
     _check(a, a2, a3, np.abs(a) + 1.0, kill)
+
+
+def test_near_unit_normalisation():
+    """unit_near1_or_zero (Snell's second tangent vector, RT:1207-1209): vectors whose norm squared lies within a few
+    ulps to 2^-31 of 1 -- where the square root and the reciprocal come from the bit pattern of the norm squared --
+    and just outside that window, with zero, tiny (below 2^-799), negative-zero and NaN components: NumPy's
+    v / |v| with NaN -> 0, bit for bit."""
+    rng = np.random.default_rng(23)
+    n = 1 << 20
+    v = rng.standard_normal((3, n))
+    v /= np.sqrt((v * v).sum(0))                                  # unit vectors, |v|^2 = 1 +- a few ulps
+    scale = np.ones(n)
+    k = rng.integers(0, 4, n)
+    scale[k == 1] = 1 + rng.uniform(-2.0 ** -32, 2.0 ** -32, (k == 1).sum())     # inside the window
+    scale[k == 2] = 1 + rng.choice([-1, 1], (k == 2).sum()) * 2.0 ** -31.5 * (1 + rng.random((k == 2).sum()))  # edge
+    scale[k == 3] = 1 + rng.uniform(-1e-3, 1e-3, (k == 3).sum())  # outside: the fallback
+    v *= scale
+    v[0, ::7] = 0.0
+    v[1, ::11] = -0.0
+    v[2, ::13] = 1e-300                                           # tiny: the quotients' slow path
+    v[0, ::17] = -np.sqrt(1 - v[1, ::17] ** 2)                    # meridional rays: one exact zero, |v| ~ 1
+    v[2, ::17] = 0.0
+    v[:, ::101] = 0.0                                             # normal incidence: 0 / 0 -> 0
+    v[1, ::103] = np.nan
+    kill = np.zeros(n, dtype=np.uint8)
+    _check(v[0], v[1], v[2], np.ones(n), kill)

@@ -79,3 +79,28 @@ def test_sphere_shell_bounds_are_exact(A):
                              A * A * (1 + rng.normal(scale=1e-13, size=200)))):
         if s >= 0:
             assert P(s) == (lo <= s <= hi)
+
+
+def test_near_unit_sqrt_and_reciprocal_bit_formulas():
+    """rtpb_math.h unit_near1_or_zero: for v = 1 + d ulps (d = bits(v) - bits(1), |d| <= 2^22, i.e. |v - 1| <= 2^-31
+    and beyond), RN(sqrt(v)) = bits(1) + (d >> 1) and RN(1 / RN(sqrt(v))) = bits(1) - 2m (m = d >> 1 >= 0) or
+    bits(1) + ceil(-m / 2) (m < 0), and d is the low word of v read as a signed 32-bit integer -- exhaustively,
+    against NumPy's correctly rounded sqrt and division."""
+    b1 = np.float64(1.0).view(np.int64)
+    d = np.arange(-(1 << 22), (1 << 22) + 1, dtype=np.int64)
+    v = (b1 + d).view(np.float64)
+    m = d >> 1
+    s = (b1 + m).view(np.float64)
+    assert np.array_equal(np.sqrt(v).view(np.int64), s.view(np.int64))
+    y = np.where(m >= 0, b1 - 2 * m, b1 + ((1 - m) >> 1)).view(np.float64)
+    assert np.array_equal((1.0 / s).view(np.int64), y.view(np.int64))
+    lo = (v.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+    assert np.array_equal(lo.astype(np.int64), d)
+    # the kernel's branch-free select for the reciprocal's offset
+    m32 = m.astype(np.int32)
+    neg = m32 >> 31
+    t = (neg & ((1 - m32) >> 1)) | (~neg & -(m32 << 1))
+    assert np.array_equal(t.astype(np.int64), np.where(m >= 0, -2 * m, (1 - m) >> 1))
+    # the window test |v - 1| <= 2^-31 keeps d inside the checked range
+    inside = np.abs(v - 1.0) <= 2.0 ** -31
+    assert np.abs(d[inside]).max() <= 1 << 22
