@@ -688,6 +688,17 @@ RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
     }
 }
 
+// (mask & a) | (~mask & b) as one v_bfi_b32 (LLVM turns the sign-splat form into a compare and a select)
+RTPB_HD int32_t bit_select(int32_t mask, int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+    return r;
+#else
+    return (mask & a) | (~mask & b);
+#endif
+}
+
 // A nearly unit vector over its norm, NaN components replaced by 0: nc = N x nb (RT:1207-1209), with N a unit normal
 // and nb a unit tangent, has |nc|^2 = |N|^2 |nb|^2 - (N . nb)^2 within a few ulps of 1 on every live row away from
 // normal incidence.  For |v - 1| <= 2^-31 the square root and the reciprocal the quotients need are read off the
@@ -705,11 +716,11 @@ RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
         const T v = x * x + y * y + z * z;
         if (__builtin_expect(tabs<T>(v - T(1)) <= T(0x1p-31), 1)) {      // v - 1 is exact (Sterbenz); NaN fails
             const int32_t d = __double2loint(v);
-            const int32_t m = d >> 1;
-            const int32_t neg = m >> 31;                                // -1 where m < 0
-            // m >= 0 ? -2m : ceil(-m / 2), as a bit select (no branch)
-            const int32_t t = (neg & ((1 - m) >> 1)) | (~neg & -(m << 1));
-            const double s = __hiloint2double(0x3FF00000 + neg, m);
+            const int32_t neg = d >> 31;                                // -1 where v < 1
+            // the reciprocal's offset, m >= 0 ? -2m : ceil(-m / 2) with m = d >> 1, in terms of d and as a bit select:
+            // d >= 0 ? -(d & ~1) : (3 - d) >> 2
+            const int32_t t = bit_select(neg, (3 - d) >> 2, -(d & ~1));
+            const double s = __hiloint2double(0x3FF00000 + neg, d >> 1);
             const double yr = __hiloint2double(0x3FF00000 + (t >> 31), t);
             div3_norm<T, G, 1>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // components at most ~1: no fixup
             return;
@@ -941,6 +952,22 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
                              static_cast<const Rcp<T>*>(nullptr), g);
 }
 
+// The front-side test d . input_axis < 0 (RT:1187-1192).  POS_ONLY (the sweep's final-position semantics) on an
+// axial surface: the sum is fma(dy, 0, dx 0) + dz, i.e. +-0 + dz, or NaN where dx or dy is infinite or NaN, so it
+// is negative exactly when dz < 0 except on rows whose dx or dy is infinite or NaN -- and those get a NaN
+// intersection and are killed by the on-surface test either way (only their unstored at-plane differs): dz < 0
+// alone.  (A class-test form of the exact test -- dz < 0 with dx, dy finite -- measured no cheaper in the history
+// kernels: the compiler then keeps register copies for the kill.)
+template <bool AX, bool POS_ONLY, typename T>
+RTPB_HD bool front_side_fails(const Ray<T>& r, const DevSurface<T>& s) {
+    if constexpr (AX && POS_ONLY) {
+        (void)s;
+        return r.dz < T(0);
+    } else {
+        return axdot<AX>(r.dx, r.dy, r.dz, s.ax[0], s.ax[1], s.ax[2]) < T(0);
+    }
+}
+
 // ------------------------------------------------------------------ one surface: (at, after)
 // Refracting surfaces RT:1160-1234, reflecting RT:1238-1303, PerfectLens RT:1601-1801.
 // One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
@@ -1002,7 +1029,7 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
-            kill_if(axdot<AX>(r.dx, r.dy, r.dz, s.ax[0], s.ax[1], s.ax[2]) < T(0), ri);
+            kill_if(front_side_fails<AX, (MODE & kPosOnly) != 0>(r, s), ri);
             emit_at(ri);
             T ratio;
             if (s.rcp_ok & 4) {

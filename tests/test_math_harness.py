@@ -96,10 +96,10 @@ def test_near_unit_sqrt_and_reciprocal_bit_formulas():
     assert np.array_equal((1.0 / s).view(np.int64), y.view(np.int64))
     lo = (v.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
     assert np.array_equal(lo.astype(np.int64), d)
-    # the kernel's branch-free select for the reciprocal's offset
-    m32 = m.astype(np.int32)
-    neg = m32 >> 31
-    t = (neg & ((1 - m32) >> 1)) | (~neg & -(m32 << 1))
+    # the kernel's branch-free select for the reciprocal's offset, written in d
+    d32 = d.astype(np.int32)
+    neg = d32 >> 31
+    t = (neg & ((3 - d32) >> 2)) | (~neg & -(d32 & ~1))
     assert np.array_equal(t.astype(np.int64), np.where(m >= 0, -2 * m, (1 - m) >> 1))
     # the window test |v - 1| <= 2^-31 keeps d inside the checked range
     inside = np.abs(v - 1.0) <= 2.0 ** -31
