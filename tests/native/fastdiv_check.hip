@@ -14,7 +14,7 @@ using namespace rtpb;
 
 namespace {
 
-constexpr int kOut = 38;
+constexpr int kOut = 39;
 
 // out: [0] div1(a, rcp(b)), [1] a / b, [2..4] div3((a, a2, a3), rcp(b)) -> x, y, z,
 //      [5] div1_as(a, bb, rcp(b)) (bb = b, or NaN where kill[i]), [6] tsqrt(b), [7] tsqrt(a),
@@ -28,7 +28,8 @@ constexpr int kOut = 38;
 //      [32..34] div3_norm((a, a2, a3), host_rcp(b, yh)) in the axial sphere normal's form: without div_fixup
 //      (SIGN = +1 / -1) where b is finite, nonzero and in the divisor range, with it elsewhere,
 //      [35..37] unit_near1_or_zero(a, a2, a3) (square root and reciprocal from the bit pattern of a norm squared
-//      within 2^-31 of 1, unit_or_zero elsewhere)
+//      within 2^-31 of 1, unit_or_zero elsewhere),
+//      [38] tsqrt_1m(1 - RN(a a))
 __global__ void check_kernel(const double* a, const double* a2, const double* a3, const double* b,
                              const double* yh, const unsigned char* kill, int64_t n, double* out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -98,6 +99,7 @@ __global__ void check_kernel(const double* a, const double* a2, const double* a3
     out[35 * n + i] = ex;
     out[36 * n + i] = ey;
     out[37 * n + i] = ez;
+    out[38 * n + i] = tsqrt_1m<double>(1.0 - ai * ai);
 }
 
 }  // namespace

@@ -76,12 +76,13 @@ def build_fastdiv():
 
 
 def fastdiv_check(a, a2, a3, b, kill):
-    """(38, n) float64: div1, a / b, div3 x/y/z, div1_as, tsqrt(b), tsqrt(a), div1 through the host's
+    """(39, n) float64: div1, a / b, div3 x/y/z, div1_as, tsqrt(b), tsqrt(a), div1 through the host's
     reciprocal RN(1/b), then the GuardDefer forms with their flags (div1, flag, div3 x/y/z, flag,
     tsqrt(b), flag, div1_as, flag), then div3_norm of (a, a2, a3) by its own norm, its GuardDefer form
     and flag, then sphere_root(a, sqrt|b|) and signed_root(a, sqrt|b|), then unit_or_zero of (a, a2, a3) and the phase
     term |(a, a2, a3)| * 2 pi / b, then the axial sphere normal's div3_norm by the host reciprocal of b (without
-    div_fixup where b is finite, nonzero and in range), then unit_near1_or_zero of (a, a2, a3) -- computed on cuda:0."""
+    div_fixup where b is finite, nonzero and in range), then unit_near1_or_zero of (a, a2, a3), then tsqrt_1m(1 - a a) --
+    computed on cuda:0."""
     global _fastdiv
     if _fastdiv is None:
         import torch  # noqa: F401 -- one HIP runtime per process: bind to torch's
@@ -93,7 +94,7 @@ def fastdiv_check(a, a2, a3, b, kill):
     arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, a2, a3, b, yh)]
     k = np.ascontiguousarray(kill, dtype=np.uint8)
     n = arrs[0].size
-    out = np.empty((38, n), dtype=np.float64)
+    out = np.empty((39, n), dtype=np.float64)
     rc = _fastdiv.fastdiv_check(*[x.ctypes.data for x in arrs], k.ctypes.data, n, out.ctypes.data)
     assert rc == 0, rc
     return out

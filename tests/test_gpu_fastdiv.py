@@ -44,6 +44,7 @@ def _check(a, a2, a3, b, kill):
         t2 = np.where(t2 < 0, np.inf, t2)
         t = np.minimum(t1, t2)
         _same(out[26], np.where(t == np.inf, np.nan, t))
+        _same(out[38], np.sqrt(1.0 - a * a))                    # tsqrt_1m: Snell's / PerfectLens' sqrt(1 - m m)
         _same(out[27], np.sign(a) * root)                       # RT:1217
         # unit_or_zero (RT:1203-1209): NumPy's v / |v| with NaN components -> 0, through the combined norm
         # test (norm2_fast) or the full sequences
