@@ -2,7 +2,7 @@
 physically contiguous buffers (hipExtMallocWithFlags(hipDeviceMallocContiguous)) and ordinary torch
 buffers, one C3 history each, then times the same C3 trace into every buffer, interleaved over rounds.
 
-    python tools/placement_alloc.py [--pairs 3] [--scale 1.0] [--flag 4]
+    python tools/placement_alloc.py [--pairs 3] [--scale 1.0] [--flag 4] [--kinds s64,s16] [--seed0 N]
 """
 import argparse
 import collections
@@ -29,7 +29,11 @@ def main():
                     help="contig (hipDeviceMallocContiguous), torch, sN (history_buffer: chunks of N MiB mapped in shuffled order)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--seed0", type=int, default=0, help="first history_buffer shuffle seed (0: the library's default sequence)")
     args = ap.parse_args()
+    if args.seed0:
+        import itertools
+        E._buffer_seed = itertools.count(args.seed0)
     dev = torch.device("cuda:0")
     lib = C.lib()
     hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
