@@ -452,20 +452,32 @@ def measure_traffic(args, config):
 
 
 F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+MIX_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT")
+# VALU issue cost per wave64 instruction (SIMD cycles): every VALU instruction issues in 4 cycles at the full rate
+# (the float64 vector peak 78.6 TFLOP/s = 1024 SIMDs x 2.4 GHz x 64 lanes x 2 FLOP / 4 cycles); a float64
+# transcendental (v_rcp_f64 / v_rsq_f64) costs 17.83 / 6.0 = 2.97 times an FMA (tools/valu/valu_rates.hip,
+# profiles/r04/g/valu_rates.log, two waves per SIMD) and does not overlap with FMAs
+ISSUE_CYCLES = {"valu": 4.0, "trans_f64": 4.0 * 17.83 / 6.0}
+SIMDS, PEAK_CLOCK_HZ = 1024, 2.4e9
 
 
 def measure_c5_flops(args):
-    """float64 FLOPs per ray of the fused sweep kernel from one PMC pass over a reduced C5 sweep (one field
-    point x 7 wavelengths x the full 10M-ray fan: the same per-ray work as the full sweep).  FLOPs =
-    64 lanes x (2 FMA + MUL + ADD + TRANS) per wave-instruction.  Also the VALU instructions per ray."""
-    vals, err = _pmc_run(args, "c5", list(F64_COUNTERS), "sweep_kernel")
+    """float64 FLOPs and the VALU instruction mix per ray of the fused sweep kernel from one PMC pass over a
+    reduced C5 sweep (one field point x 7 wavelengths x the full 10M-ray fan: the same per-ray work as the full
+    sweep).  FLOPs = 64 lanes x (2 FMA + MUL + ADD + TRANS) per wave-instruction.  The mix gives the sweep's
+    issue-time ceiling: every VALU instruction at ISSUE_CYCLES on 1024 SIMDs at 2.4 GHz."""
+    vals, err = _pmc_run(args, "c5", list(F64_COUNTERS) + list(MIX_COUNTERS), "sweep_kernel")
     if err:
         return None, err
     tot = {k: sum(v) for k, v in vals.items()}
     flops = 64.0 * (2 * tot["SQ_INSTS_VALU_FMA_F64"] + tot["SQ_INSTS_VALU_MUL_F64"] + tot["SQ_INSTS_VALU_ADD_F64"] +
                     tot["SQ_INSTS_VALU_TRANS_F64"])
     rays = 7 * C5_FAN[0] * C5_FAN[1]
-    return {"flops_per_ray": flops / rays, "f64_wave_instructions": tot, "pmc_sample_rays": rays}, None
+    trans = tot["SQ_INSTS_VALU_TRANS_F64"]
+    cycles = (tot["SQ_INSTS_VALU"] - trans) * ISSUE_CYCLES["valu"] + trans * ISSUE_CYCLES["trans_f64"]
+    return {"flops_per_ray": flops / rays, "f64_wave_instructions": {k: tot[k] for k in F64_COUNTERS},
+            "valu_mix_wave_instructions": {k: tot[k] for k in MIX_COUNTERS}, "pmc_sample_rays": rays,
+            "issue_simd_cycles_per_ray": cycles / rays}, None
 
 
 def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None, copy=None):
@@ -542,6 +554,14 @@ def run_c2(args, dev, copy):
     res = {"baseline_config": "configs[1]", "workload": w2.workload, "dtype": "f64", "storage": w2.storage,
            "value": w2.n * w2.S * steps / e2, "unit": UNIT, "n_gpus": 1, "steps": steps, "ms_per_step": e2 / steps * 1e3,
            "rays": w2.n, "surfaces": w2.S, "roofline": roofline(w2, k2, tr2, note2, w2.fill_rate(), copy)}
+    # the drop-in call with its default history allocation (System.ray_trace on the device bundle, no out=)
+    e2e_ms, e2e_kernel_ms = w2.e2e(reps=31)
+    res.update(e2e_ms=e2e_ms, e2e_kernel_ms=e2e_kernel_ms, e2e_overhead_ms=e2e_ms - e2e_kernel_ms,
+               e2e_over_loop_kernel=e2e_ms / k2,
+               e2e_note="System.ray_trace(torch rays, Vacuum(), Vacuum()) on the device-resident C2 bundle, the median "
+                        "of 31 calls: lowering (memoised), history allocation (the default: the history pool's "
+                        "shuffled-chunk memory, reused through torch's caching allocator), launch, synchronise; "
+                        "e2e_kernel_ms: the same call's kernel (HIP events)")
     res["host_e2e"] = host_e2e(w2)
     del w2
     torch.cuda.empty_cache()
@@ -639,11 +659,26 @@ def run_c5(args, dev, rank, world):
         fl, err = measure_c5_flops(args)
         if fl:
             rays0 = g[0][2]
+            S14 = len(system.surfaces)
+            mix = fl["valu_mix_wave_instructions"]
+            per_rs = lambda v: v * 64.0 / (fl["pmc_sample_rays"] * S14)       # wave-instructions -> per ray-surface
+            issue_s = fl["issue_simd_cycles_per_ray"] * rays0 / SIMDS / PEAK_CLOCK_HZ
             rl.update(achieved=fl["flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
                       flops_per_ray=fl["flops_per_ray"], f64_wave_instructions_sample=fl["f64_wave_instructions"],
                       pmc_sample_rays=fl["pmc_sample_rays"],
                       flops_method="PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes (FMA = 2) on a 1-field "
-                                   "sweep, scaled per ray")
+                                   "sweep, scaled per ray",
+                      valu_per_ray_surface=per_rs(mix["SQ_INSTS_VALU"]),
+                      valu_mix_per_ray_surface={
+                          "f64_add_mul_fma": per_rs(sum(fl["f64_wave_instructions"][k] for k in F64_COUNTERS[:3])),
+                          "f64_trans": per_rs(fl["f64_wave_instructions"]["SQ_INSTS_VALU_TRANS_F64"]),
+                          "int32": per_rs(mix["SQ_INSTS_VALU_INT32"]), "int64": per_rs(mix["SQ_INSTS_VALU_INT64"]),
+                          "cvt": per_rs(mix["SQ_INSTS_VALU_CVT"])},
+                      issue_ceiling_s=issue_s, frac_issue=issue_s / (g[0][1] * 1e-3),
+                      issue_method=("PMC VALU wave-instructions of the 1-field sample scaled to the rank's rays, each at "
+                                    "4 SIMD cycles (the full wave64 rate: 78.6 TF f64 = 1024 SIMDs x 2.4 GHz x 64 x 2 / "
+                                    "4) and a float64 transcendental at 2.97x (tools/valu/valu_rates.hip), over 1024 "
+                                    "SIMDs at 2.4 GHz; frac_issue = that ceiling / the measured kernel time"))
             rl["frac"] = rl["achieved"] / F64_VALU_PEAK_TFLOPS
         else:
             rl["flops_note"] = err

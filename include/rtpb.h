@@ -39,12 +39,16 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 6   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+#define RTPB_ABI_VERSION 7   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
                                 3: input element type separate from the storage type (in_dtype)
                                 4: + rtpb_trace_checked (table-miss flag)
                                 5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers)
                                 6: stream-ordered history buffers: rtpb_buffer_alloc takes the stream,
-                                   + rtpb_buffer_record_stream / _held / _dlpack_discard */
+                                   + rtpb_buffer_record_stream / _held / _dlpack_discard
+                                7: + rtpb_torch_alloc / rtpb_torch_free (torch MemPool segments),
+                                   rtpb_buffer_stats; releasing a mapping synchronises the device;
+                                   + rtpb_ray_fan_tables_wl / rtpb_collimated_rays_tables_wl (per-ray
+                                   wavelengths) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -154,6 +158,23 @@ int rtpb_buffer_held(int32_t device, uint64_t* bytes, int32_t* buffers);
 int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed);
 int rtpb_buffer_dlpack_discard(void* managed);
 
+/* ---- torch MemPool segments (ABI 7) ------------------------------------------------------------- */
+/* The same shuffled-chunk memory as the segment allocator of PyTorch's caching allocator:
+       torch.cuda.MemPool(torch.cuda.memory.CUDAPluggableAllocator("librtpb.so", "rtpb_torch_alloc",
+                                                                    "rtpb_torch_free").allocator())
+   (torch's alloc_fn / free_fn signatures: void* (size_t, int, hipStream_t), void (void*, size_t, int,
+   hipStream_t)).  torch then caches, reuses stream-ordered (Tensor.record_stream), counts
+   (torch.cuda.memory_allocated) and releases (empty_cache / out of memory) those segments itself; the library
+   only maps a fresh buffer of `size` bytes (NULL on failure) and, on free, synchronises the device and unmaps
+   it.  ray_trace_pb_amd's default device histories come from such a pool (_engine.history_pool).
+   rtpb_buffer_stats fills up to n of: [0] live torch-pool segment bytes on `device` (-1: all), [1] their
+   count, [2] reserved virtual bytes of released mappings (never reused), [3] their count,
+   [4] buffers allocated with plain hipMalloc because [2] reached rtpb_set_tuning("buffer_dead_va_limit"),
+   [5] torch segments allocated, [6] torch segments freed, [7] the dead-VA limit in bytes. */
+void* rtpb_torch_alloc(int64_t size, int32_t device, void* stream);
+void rtpb_torch_free(void* ptr, int64_t size, int32_t device, void* stream);
+int rtpb_buffer_stats(int32_t device, uint64_t* out, int32_t n);
+
 /* ---- plans: reference System + initial/final materials, lowered ----------------------------- */
 /* Validates and stores the system.  `nmat` must equal `nsurf + 1` (RT:653-656: initial material,
    System.materials, final material).  `dtype` is the STORAGE type of the output history, RTPB_F64 or
@@ -225,6 +246,18 @@ int rtpb_ray_fan_tables(int32_t device, int32_t dtype, void* rays_out, const dou
 int rtpb_collimated_rays_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_disps,
                                 int64_t nphis, const double normal[3], const double n1[3], const double n2[3],
                                 const double* offsets, const double* phi_cos_sin, double wavelength, void* stream);
+/* ABI 7: the same with one wavelength per ray -- the reference's "either floating point or an array the same
+   size as n_disps * nphis" (RT:115; rays[:, 7] = wavelengths, RT:94 / RT:159).  `wavelengths` is a DEVICE
+   pointer to n_thetas*nphis (n_disps*nphis) float64 values in ray-index order, 8-byte aligned, read by the
+   kernel (stream-ordered); everything else as above. */
+int rtpb_ray_fan_tables_wl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_thetas,
+                           int64_t nphis, const double center_ray[3], const double ex[3], const double ey[3],
+                           const double* theta_cos_sin, const double* phi_cos_sin, const double* wavelengths,
+                           void* stream);
+int rtpb_collimated_rays_tables_wl(int32_t device, int32_t dtype, void* rays_out, const double pt[3],
+                                   int64_t n_disps, int64_t nphis, const double normal[3], const double n1[3],
+                                   const double n2[3], const double* offsets, const double* phi_cos_sin,
+                                   const double* wavelengths, void* stream);
 
 /* propagate_ray2plane(rays, normal, center, material, exclude_backward_propagation) (RT:241-306) on
    device rays (AOS n x 8).  normal / center: DEVICE pointers to 3 doubles (broadcast) or n x 3 doubles
@@ -329,7 +362,9 @@ int rtpb_distinct_keys(int32_t device, const void* col, int32_t dtype, int64_t n
    key set (and that have no POLY6 material) also tabulate every other material at those keys, so the
    kernel reads n from LDS instead of evaluating Sellmeier dispersion per surface (bit-identical: the
    host evaluates the kernel's own material_n); 0 = evaluate per surface.
-   "buffer_pool_buffers": freed history buffers kept mapped per device for reuse (default 1, 0..1024). */
+   "buffer_pool_buffers": freed history buffers kept mapped per device for reuse (default 1, 0..1024).
+   "buffer_dead_va_limit": reserved virtual bytes of released buffer mappings (never reused) beyond which new
+                           history buffers are plain hipMalloc allocations (default 32 TiB). */
 int rtpb_set_tuning(const char* key, int64_t value);
 
 /* ---- kernel timing (benchmarks) ------------------------------------------------------------- */

@@ -11,7 +11,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 6
+RTPB_ABI_VERSION = 7
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
@@ -60,6 +60,9 @@ SIGNATURES = {
     "rtpb_buffer_held": (ctypes.c_int, [_i32, ctypes.POINTER(_u64), ctypes.POINTER(_i32)]),
     "rtpb_buffer_dlpack": (ctypes.c_int, [_P, _i32, ctypes.POINTER(_i64), _i32, ctypes.POINTER(_P)]),
     "rtpb_buffer_dlpack_discard": (ctypes.c_int, [_P]),
+    "rtpb_torch_alloc": (ctypes.c_void_p, [_i64, _i32, _P]),
+    "rtpb_torch_free": (None, [_P, _i64, _i32, _P]),
+    "rtpb_buffer_stats": (ctypes.c_int, [_i32, ctypes.POINTER(_u64), _i32]),
     "rtpb_plan_create": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _i32,
                                         ctypes.POINTER(_P)]),
     "rtpb_plan_destroy": (ctypes.c_int, [_P]),
@@ -77,6 +80,8 @@ SIGNATURES = {
     "rtpb_ray_fan_tables": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P, ctypes.c_double, _P]),
     "rtpb_collimated_rays_tables": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P,
                                                    ctypes.c_double, _P]),
+    "rtpb_ray_fan_tables_wl": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _P]),
+    "rtpb_collimated_rays_tables_wl": (ctypes.c_int, [_i32, _i32, _P, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _P]),
     "rtpb_spot_sweep": (ctypes.c_int, [_P, _i32, _i64, _P, _i64, _i64, _P, _P, _P, _P, _P, _P, _i64, _P, _P]),
     "rtpb_grid_interpolate": (ctypes.c_int, [_i32, ctypes.POINTER(Triangulation), _P, _i64, _P, _i64,
                                              ctypes.c_double, _P, _P, _P]),

@@ -509,6 +509,54 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
         raise
 
 
+_POOLS = {}
+_ALLOCATORS = {}            # the pools hold a raw pointer to their allocator: keep it alive with the pool
+_pools_lock = threading.Lock()
+
+
+def history_pool(device_index):
+    """The torch.cuda.MemPool of device ``device_index``'s history buffers: torch's caching allocator with
+    librtpb's shuffled-chunk mappings as its segment allocator (rtpb_torch_alloc / rtpb_torch_free, ABI 7).
+    torch owns everything else -- caching, stream-ordered reuse (Tensor.record_stream), memory statistics and
+    out-of-memory handling; ``use_on_oom``: an allocation outside the pool that runs out of memory may take
+    the pool's cached blocks."""
+    import torch
+    idx = int(device_index)
+    with _pools_lock:
+        pool = _POOLS.get(idx)
+        if pool is None:
+            C.lib()                 # loaded after torch: the allocator binds to torch's HIP runtime
+            alloc = torch.cuda.memory.CUDAPluggableAllocator(C.LIB_PATH, "rtpb_torch_alloc", "rtpb_torch_free")
+            with torch.cuda.device(idx):
+                pool = torch.cuda.MemPool(alloc.allocator(), use_on_oom=True)
+            _ALLOCATORS[idx] = alloc
+            _POOLS[idx] = pool
+    return pool
+
+
+def pool_empty(shape, dtype, device, stream=None):
+    """torch.empty(shape, dtype, device) allocated in the device's history pool (:func:`history_pool`) for
+    ``stream`` (default: the current stream)."""
+    import torch
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = history_pool(idx)
+    with torch.cuda.device(idx):
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx, torch.cuda.use_mem_pool(pool, idx):
+            return torch.empty(shape, dtype=dtype, device=torch.device("cuda", idx))
+
+
+def buffer_stats(device=-1):
+    """librtpb's buffer statistics (rtpb_buffer_stats): live torch-pool segment bytes and count, dead virtual
+    bytes and ranges, plain-allocation fallbacks, torch segments allocated / freed, the dead-VA limit."""
+    out = (ctypes.c_uint64 * 8)()
+    C.check(C.lib().rtpb_buffer_stats(int(device), out, 8))
+    keys = ("pool_bytes", "pool_segments", "dead_va_bytes", "dead_va_ranges", "plain_allocs", "segments_allocated",
+            "segments_freed", "dead_va_limit")
+    return dict(zip(keys, (int(v) for v in out)))
+
+
 def record_stream(tensor, stream):
     """``tensor.record_stream(stream)`` for every kind of device memory: torch's caching-allocator record,
     plus the library's record when the tensor lies in a history buffer (rtpb_buffer_record_stream) -- torch

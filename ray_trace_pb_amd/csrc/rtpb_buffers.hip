@@ -25,9 +25,22 @@
 //     range kept reserved) once its events have completed -- checked without blocking on every
 //     later alloc / free, and waited for by rtpb_buffer_trim, rtpb_shutdown and an allocation that finds the
 //     device full.
+//
+// torch's own caching allocator can use the same memory (ABI 7): rtpb_torch_alloc / rtpb_torch_free are the
+// allocation functions of a torch.cuda.memory.CUDAPluggableAllocator behind a torch.cuda.MemPool
+// (ray_trace_pb_amd._engine.history_pool).  torch then owns streams, caching, record_stream, statistics and
+// out-of-memory handling of those segments; the library only maps (alloc) and unmaps (free) them.
+//
+// Releasing a mapping always synchronises the device first: torch frees without a device sync, and a use on a
+// stream never recorded may still be in flight (HIP's unmap, unlike hipFree, does not wait for it).  The
+// virtual range of a buffer a kernel may have used is kept reserved (a range freed and reserved
+// again took writes through its old translations in round 4); those dead ranges are counted
+// (rtpb_buffer_stats), and once they exceed rtpb_set_tuning("buffer_dead_va_limit", bytes) new buffers are
+// plain hipMalloc allocations (correct, without the shuffled placement).
 #include "rtpb_internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -40,6 +53,7 @@ struct Buffer {
     int dev = 0;
     void* va = nullptr;
     size_t size = 0, chunk = 0;
+    bool plain = false;                                    // hipMalloc'd (dead-VA budget spent): hipFree
     std::vector<hipMemGenericAllocationHandle_t> chunks;   // created physical chunks
     std::vector<uint64_t> mapped;                          // virtual slot of each mapped chunk
     hipStream_t alloc_stream = nullptr;                    // the stream the current owner allocated it for
@@ -52,6 +66,11 @@ std::map<uintptr_t, Buffer*> g_live;             // buffers owned by a caller, b
 std::vector<Buffer*> g_pool;                     // freed, still mapped, ready for reuse (newest last)
 std::vector<Buffer*> g_retired;                  // freed, leaving the pool: destroyed once `pending` is done
 size_t g_pool_keep = 1;                          // pooled buffers kept per device
+std::map<uintptr_t, Buffer*> g_torch;            // live segments of torch MemPools (rtpb_torch_alloc)
+uint64_t g_dead_va = 0;                          // reserved virtual bytes of released mappings (never reused)
+uint64_t g_dead_ranges = 0, g_plain = 0, g_torch_allocs = 0, g_torch_frees = 0;
+uint64_t g_dead_va_limit = 32ull << 40;          // beyond this, new buffers are plain hipMalloc allocations
+std::atomic<uint64_t> g_torch_seed{0x7a11};      // shuffle seeds of torch-pool segments
 
 int stream_device(hipStream_t s, int fallback) {
     int d = fallback;
@@ -71,20 +90,36 @@ void drop_events(Buffer* b) {
 }
 
 // Unmaps and releases the physical chunks of a buffer, after waiting for the recorded uses of its last owner
-// (b->pending); its virtual range stays reserved and unused.  The Buffer object is deleted.
-int destroy(Buffer* b) {
+// (b->pending) and for the whole device: a use on a stream nobody recorded may still be in flight, and an
+// unmap does not wait for it.  `used`: a kernel may have touched the memory -- its virtual range then stays
+// reserved (counted in g_dead_va); a buffer no kernel saw (an allocation that failed half way) frees it.
+// The Buffer object is deleted.
+int destroy(Buffer* b, bool used = true) {
     DeviceGuard g(b->dev);
     hipError_t e = hipSuccess;
     for (hipEvent_t ev : b->pending)
         if (hipEventSynchronize(ev) != hipSuccess) e = hipErrorUnknown;
     drop_events(b);
-    for (uint64_t s : b->mapped)
-        if (hipMemUnmap(static_cast<char*>(b->va) + s * b->chunk, b->chunk) != hipSuccess) e = hipErrorUnknown;
-    for (auto h : b->chunks)
-        if (hipMemRelease(h) != hipSuccess) e = hipErrorUnknown;
-    // The virtual range is NOT freed: a range freed and reserved again by a later buffer was seen to take
-    // writes through translations still cached for the old mapping (partial histories, profiles/r04/
-    // buffers_va_reuse.log).  Kept reserved it is never touched again; the cost is address space only.
+    if (used && hipDeviceSynchronize() != hipSuccess) e = hipErrorUnknown;
+    if (b->plain) {
+        if (b->va && hipFree(b->va) != hipSuccess) e = hipErrorUnknown;
+    } else {
+        for (uint64_t s : b->mapped)
+            if (hipMemUnmap(static_cast<char*>(b->va) + s * b->chunk, b->chunk) != hipSuccess) e = hipErrorUnknown;
+        for (auto h : b->chunks)
+            if (hipMemRelease(h) != hipSuccess) e = hipErrorUnknown;
+        if (b->va && !used) {
+            if (hipMemAddressFree(b->va, b->size) != hipSuccess) e = hipErrorUnknown;
+        } else if (b->va) {
+            // The virtual range is NOT freed: a range freed and reserved again by a later buffer was seen to
+            // take writes through translations still cached for the old mapping (partial histories,
+            // profiles/r04/buffers_va_reuse.log).  Kept reserved it is never touched again; the cost is
+            // address space, counted here and bounded by g_dead_va_limit.
+            std::lock_guard<std::mutex> lk(g_mu);
+            g_dead_va += b->size;
+            ++g_dead_ranges;
+        }
+    }
     delete b;
     return e == hipSuccess ? RTPB_OK : fail(RTPB_E_HIP, "rtpb_buffer: releasing a mapping failed");
 }
@@ -264,45 +299,81 @@ int set_buffer_pool_keep(int64_t k) {
     }
     return RTPB_OK;
 }
+
+// rtpb_set_tuning("buffer_dead_va_limit", bytes): reserved virtual bytes of released mappings before new
+// buffers fall back to plain hipMalloc allocations
+int set_buffer_dead_va_limit(int64_t bytes) {
+    if (bytes < 0) return fail(RTPB_E_INVALID, "rtpb_set_tuning: buffer_dead_va_limit must be >= 0");
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_dead_va_limit = static_cast<uint64_t>(bytes);
+    return RTPB_OK;
+}
 }  // namespace rtpbi
 
-extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void* stream,
-                                 void** ptr, void** handle) {
-    if (!ptr || !handle || bytes == 0 || bytes > (1ull << 50))
-        return fail(RTPB_E_INVALID, "rtpb_buffer_alloc: null output, zero size or more than 1 PiB");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
-        return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
-    const auto st = static_cast<hipStream_t>(stream);
-    DeviceGuard g(device);
+namespace {
+
+hipMemAllocationProp device_prop(int32_t device) {
     hipMemAllocationProp prop = {};
     prop.type = hipMemAllocationTypePinned;
     prop.location.type = hipMemLocationTypeDevice;
     prop.location.id = device;
+    return prop;
+}
+
+// Chunk size and count of a buffer of `bytes` (`chunk_bytes` 0: 64 MiB; a buffer smaller than one chunk is a
+// single chunk of its own size, rounded to the allocation granularity); the caller has set the device.
+int chunk_geometry(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t* chunk, uint64_t* n,
+                   uint64_t* gran_out = nullptr) {
+    hipMemAllocationProp prop = device_prop(device);
     size_t gran = 0;
     HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
     gran = std::max<size_t>(gran, 1);
     auto round_up = [](uint64_t v, uint64_t m) { return (v + m - 1) / m * m; };
     const uint64_t want = chunk_bytes ? chunk_bytes : (64ull << 20);
-    // a buffer smaller than one chunk is a single chunk of its own (rounded) size
-    const uint64_t chunk = round_up(std::min<uint64_t>(want, round_up(bytes, gran)), gran);
-    const uint64_t n = (bytes + chunk - 1) / chunk;
-    if (Buffer* p = take_pooled(device, n * chunk, chunk, st)) {
-        own(p, st);
-        *ptr = p->va;
-        *handle = p;
-        return RTPB_OK;
-    }
+    *chunk = round_up(std::min<uint64_t>(want, round_up(bytes, gran)), gran);
+    *n = (bytes + *chunk - 1) / *chunk;
+    if (gran_out) *gran_out = gran;
+    return RTPB_OK;
+}
+
+// A new buffer of at least `bytes` on `device`: physical chunks mapped in a shuffled order into a fresh
+// virtual range -- or, once the dead virtual ranges exceed g_dead_va_limit, one plain hipMalloc allocation.
+// Out of device memory, the library's pooled and retired buffers of the device are released once and the
+// allocation retried.
+int map_new(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, Buffer** out) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
+    DeviceGuard g(device);
+    const hipMemAllocationProp prop = device_prop(device);
+    uint64_t chunk = 0, n = 0, gran = 1;
+    const int rc = chunk_geometry(device, bytes, chunk_bytes, &chunk, &n, &gran);
+    if (rc != RTPB_OK) return rc;
     auto* b = new Buffer;
     b->dev = device;
     b->size = n * chunk;
     b->chunk = chunk;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        b->plain = g_dead_va + b->size > g_dead_va_limit;
+        g_plain += b->plain;
+    }
+    if (b->plain) {
+        if (hipMalloc(&b->va, b->size) != hipSuccess &&
+            (trim_pool(device) != RTPB_OK || hipMalloc(&b->va, b->size) != hipSuccess)) {
+            b->va = nullptr;
+            (void)destroy(b, false);
+            return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMalloc failed (out of device memory?)");
+        }
+        *out = b;
+        return RTPB_OK;
+    }
     // chunk-aligned virtual range when the chunk is a power of two (large translation fragments), else the
     // allocation granularity (a small buffer's single chunk)
     const uint64_t align = (chunk & (chunk - 1)) == 0 ? chunk : gran;
     if (hipMemAddressReserve(&b->va, b->size, align, nullptr, 0) != hipSuccess) {
         b->va = nullptr;
-        (void)destroy(b);
+        (void)destroy(b, false);
         return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemAddressReserve failed");
     }
     std::vector<uint64_t> slot(n);
@@ -317,14 +388,14 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
         if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
             // out of memory: release the pooled and retired buffers of this device once and retry
             if (trimmed || trim_pool(device) != RTPB_OK || hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
-                (void)destroy(b);
+                (void)destroy(b, false);
                 return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemCreate failed (out of device memory?)");
             }
             trimmed = true;
         }
         b->chunks.push_back(h);
         if (hipMemMap(static_cast<char*>(b->va) + slot[k] * chunk, chunk, 0, h, 0) != hipSuccess) {
-            (void)destroy(b);
+            (void)destroy(b, false);
             return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemMap failed");
         }
         b->mapped.push_back(slot[k]);
@@ -333,12 +404,90 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;
     if (hipMemSetAccess(b->va, b->size, &acc, 1) != hipSuccess) {
-        (void)destroy(b);
+        (void)destroy(b, false);
         return fail(RTPB_E_HIP, "rtpb_buffer_alloc: hipMemSetAccess failed");
     }
+    *out = b;
+    return RTPB_OK;
+}
+
+}  // namespace
+
+extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, void* stream,
+                                 void** ptr, void** handle) {
+    if (!ptr || !handle || bytes == 0 || bytes > (1ull << 50))
+        return fail(RTPB_E_INVALID, "rtpb_buffer_alloc: null output, zero size or more than 1 PiB");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
+    const auto st = static_cast<hipStream_t>(stream);
+    {
+        DeviceGuard g(device);
+        uint64_t chunk = 0, n = 0;
+        const int rc = chunk_geometry(device, bytes, chunk_bytes, &chunk, &n);
+        if (rc != RTPB_OK) return rc;
+        if (Buffer* p = take_pooled(device, n * chunk, chunk, st)) {
+            own(p, st);
+            *ptr = p->va;
+            *handle = p;
+            return RTPB_OK;
+        }
+    }
+    Buffer* b = nullptr;
+    const int rc = map_new(device, bytes, chunk_bytes, seed, &b);
+    if (rc != RTPB_OK) return rc;
     own(b, st);
     *ptr = b->va;
     *handle = b;
+    return RTPB_OK;
+}
+
+// torch.cuda.memory.CUDAPluggableAllocator(librtpb.so, "rtpb_torch_alloc", "rtpb_torch_free"): a segment of a
+// torch MemPool -- a fresh shuffled-chunk mapping (torch's caching allocator caches and reuses it).  NULL on
+// failure (torch then frees its cached blocks and retries, or raises its out-of-memory error).
+extern "C" void* rtpb_torch_alloc(int64_t size, int32_t device, void* stream) {
+    (void)stream;
+    if (size <= 0) return nullptr;
+    Buffer* b = nullptr;
+    if (map_new(device, static_cast<uint64_t>(size), 0, g_torch_seed.fetch_add(1), &b) != RTPB_OK) return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_torch[reinterpret_cast<uintptr_t>(b->va)] = b;
+    ++g_torch_allocs;
+    return b->va;
+}
+
+extern "C" void rtpb_torch_free(void* ptr, int64_t size, int32_t device, void* stream) {
+    (void)size, (void)device, (void)stream;
+    Buffer* b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_torch.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it == g_torch.end()) return;
+        b = it->second;
+        g_torch.erase(it);
+        ++g_torch_frees;
+    }
+    (void)destroy(b);
+}
+
+extern "C" int rtpb_buffer_stats(int32_t device, uint64_t* out, int32_t n) {
+    if (!out || n < 0) return fail(RTPB_E_INVALID, "rtpb_buffer_stats: null output");
+    uint64_t v[8] = {};
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (const auto& kv : g_torch)
+            if (device < 0 || kv.second->dev == device) {
+                v[0] += kv.second->size;
+                ++v[1];
+            }
+        v[2] = g_dead_va;
+        v[3] = g_dead_ranges;
+        v[4] = g_plain;
+        v[5] = g_torch_allocs;
+        v[6] = g_torch_frees;
+        v[7] = g_dead_va_limit;
+    }
+    for (int32_t k = 0; k < n && k < 8; ++k) out[k] = v[k];
     return RTPB_OK;
 }
 

@@ -42,6 +42,7 @@ struct FanArgs {
     int64_t n_thetas, nphis;
     double pt[3], c[3], ex[3], ey[3];
     double wl;
+    const double* __restrict__ wls;     // per-ray wavelengths (device, ray-index order) or NULL: `wl` for all
 };
 
 template <typename T>
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(kTraceBlock) void ray_fan_kernel(FanArgs<T> a) {
         r.dy = a.c[1] * ct + a.ex[1] * cp * st + a.ey[1] * sp * st;
         r.dz = a.c[2] * ct + a.ex[2] * cp * st + a.ey[2] * sp * st;
         r.ph = 0.0;
-        r.wl = a.wl;
+        r.wl = a.wls ? a.wls[k] : a.wl;                  // rays[:, 7] = wavelengths (RT:94)
         tile_write<T>(tile, lane, r);
     }
     lds_wait();
@@ -77,6 +78,7 @@ struct CollArgs {
     int64_t n_disps, nphis;
     double pt[3], n1[3], n2[3], nrm[3];
     double start, stop, step, wl;
+    const double* __restrict__ wls;     // per-ray wavelengths (device, ray-index order) or NULL: `wl` for all
     int32_t use_offsets;                // 1: offset of idisp = tab[idisp].x (the caller's np.linspace)
 };
 
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(kTraceBlock) void collimated_kernel(CollArgs a) {
         r.z = a.pt[2] + a.n1[2] * oc + a.n2[2] * os;
         r.dx = a.nrm[0]; r.dy = a.nrm[1]; r.dz = a.nrm[2];
         r.ph = 0.0;
-        r.wl = a.wl;
+        r.wl = a.wls ? a.wls[k] : a.wl;                  // rays[:, 7] = wavelengths (RT:159)
         tile_write<T>(tile, lane, r);
     }
     lds_wait();
@@ -135,9 +137,10 @@ int gen_tables(double2** tab, int64_t n_a, int64_t n_b, const double* host_a, co
 
 int fan_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max, int64_t n_thetas,
              int64_t nphis, const double c[3], const double* ex_in, const double* ey_in, const double* theta_cs,
-             const double* phi_cs, double wavelength, void* stream) {
+             const double* phi_cs, double wavelength, const double* wls, void* stream) {
     int rc = check_device(device);
     if (rc) return rc;
+    if (reinterpret_cast<uintptr_t>(wls) % 8) return fail(RTPB_E_INVALID, "wavelengths must be 8-byte aligned");
     if (n_thetas <= 0 || nphis <= 0 || !rays_out || !pt || !c) return fail(RTPB_E_INVALID, "bad ray-fan arguments");
     if ((theta_cs == nullptr) != (phi_cs == nullptr)) return fail(RTPB_E_INVALID, "pass both trig tables or neither");
     if (reinterpret_cast<uintptr_t>(rays_out) % 16) return fail(RTPB_E_INVALID, "rays_out must be 16-byte aligned");
@@ -178,6 +181,7 @@ int fan_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], 
             a.pt[j] = pt[j]; a.c[j] = c[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
         }
         a.wl = wavelength;
+        a.wls = wls;
         hipLaunchKernelGGL(ray_fan_kernel<T>, dim3(blocks), dim3(kTraceBlock), 0, st, a);
     };
     if (dtype == RTPB_F64) go(double{});
@@ -190,9 +194,10 @@ int fan_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], 
 int collimated_impl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
                     int64_t n_disps, int64_t nphis, double phi_start, const double nv[3], const double* n1_in,
                     const double* n2_in, const double* offsets, const double* phi_cs, double wavelength,
-                    void* stream) {
+                    const double* wls, void* stream) {
     int rc = check_device(device);
     if (rc) return rc;
+    if (reinterpret_cast<uintptr_t>(wls) % 8) return fail(RTPB_E_INVALID, "wavelengths must be 8-byte aligned");
     if (n_disps <= 0 || nphis <= 0 || !rays_out || !pt || !nv)
         return fail(RTPB_E_INVALID, "bad collimated-ray arguments");
     if ((offsets == nullptr) != (phi_cs == nullptr)) return fail(RTPB_E_INVALID, "pass both tables or neither");
@@ -228,6 +233,7 @@ int collimated_impl(int32_t device, int32_t dtype, void* rays_out, const double 
     a.step = n_disps > 1 ? (displacement_max - (-displacement_max)) / double(n_disps - 1) : 0.0;
     a.use_offsets = offsets != nullptr;
     a.wl = wavelength;
+    a.wls = wls;
     DeviceGuard g(device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     TrigArgs ta{};
@@ -254,7 +260,7 @@ extern "C" {
 int rtpb_ray_fan(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double theta_max,
                  int64_t n_thetas, int64_t nphis, const double center_ray[3], double wavelength, void* stream) {
     return fan_impl(device, dtype, rays_out, pt, theta_max, n_thetas, nphis, center_ray, nullptr, nullptr, nullptr,
-                    nullptr, wavelength, stream);
+                    nullptr, wavelength, nullptr, stream);
 }
 
 int rtpb_ray_fan_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_thetas,
@@ -262,14 +268,24 @@ int rtpb_ray_fan_tables(int32_t device, int32_t dtype, void* rays_out, const dou
                         const double* theta_cos_sin, const double* phi_cos_sin, double wavelength, void* stream) {
     if (!ex || !ey || !theta_cos_sin || !phi_cos_sin) return fail(RTPB_E_INVALID, "NULL table argument");
     return fan_impl(device, dtype, rays_out, pt, 0.0, n_thetas, nphis, center_ray, ex, ey, theta_cos_sin, phi_cos_sin,
-                    wavelength, stream);
+                    wavelength, nullptr, stream);
+}
+
+int rtpb_ray_fan_tables_wl(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_thetas,
+                           int64_t nphis, const double center_ray[3], const double ex[3], const double ey[3],
+                           const double* theta_cos_sin, const double* phi_cos_sin, const double* wavelengths,
+                           void* stream) {
+    if (!ex || !ey || !theta_cos_sin || !phi_cos_sin || !wavelengths)
+        return fail(RTPB_E_INVALID, "NULL table or wavelength argument");
+    return fan_impl(device, dtype, rays_out, pt, 0.0, n_thetas, nphis, center_ray, ex, ey, theta_cos_sin, phi_cos_sin,
+                    0.0, wavelengths, stream);
 }
 
 int rtpb_collimated_rays(int32_t device, int32_t dtype, void* rays_out, const double pt[3], double displacement_max,
                          int64_t n_disps, int64_t nphis, double phi_start, const double normal[3], double wavelength,
                          void* stream) {
     return collimated_impl(device, dtype, rays_out, pt, displacement_max, n_disps, nphis, phi_start, normal, nullptr,
-                           nullptr, nullptr, nullptr, wavelength, stream);
+                           nullptr, nullptr, nullptr, wavelength, nullptr, stream);
 }
 
 int rtpb_collimated_rays_tables(int32_t device, int32_t dtype, void* rays_out, const double pt[3], int64_t n_disps,
@@ -277,7 +293,17 @@ int rtpb_collimated_rays_tables(int32_t device, int32_t dtype, void* rays_out, c
                                 const double* offsets, const double* phi_cos_sin, double wavelength, void* stream) {
     if (!n1 || !n2 || !offsets || !phi_cos_sin) return fail(RTPB_E_INVALID, "NULL table argument");
     return collimated_impl(device, dtype, rays_out, pt, 0.0, n_disps, nphis, 0.0, normal, n1, n2, offsets, phi_cos_sin,
-                           wavelength, stream);
+                           wavelength, nullptr, stream);
+}
+
+int rtpb_collimated_rays_tables_wl(int32_t device, int32_t dtype, void* rays_out, const double pt[3],
+                                   int64_t n_disps, int64_t nphis, const double normal[3], const double n1[3],
+                                   const double n2[3], const double* offsets, const double* phi_cos_sin,
+                                   const double* wavelengths, void* stream) {
+    if (!n1 || !n2 || !offsets || !phi_cos_sin || !wavelengths)
+        return fail(RTPB_E_INVALID, "NULL table or wavelength argument");
+    return collimated_impl(device, dtype, rays_out, pt, 0.0, n_disps, nphis, 0.0, normal, n1, n2, offsets, phi_cos_sin,
+                           0.0, wavelengths, stream);
 }
 
 }  // extern "C"

@@ -95,6 +95,7 @@ extern template hipError_t launch_trace<float, double>(const TraceArgs<float, do
 // tuning knobs (rtpb_set_tuning, defined in rtpb_trace.hip)
 extern std::atomic<int> g_aos_staging, g_nt_stores, g_stage_input, g_host_chunk_mib, g_indexed_materials;
 int set_buffer_pool_keep(int64_t k);              // rtpb_buffers.hip: rtpb_set_tuning("buffer_pool_buffers")
+int set_buffer_dead_va_limit(int64_t bytes);     // rtpb_buffers.hip: rtpb_set_tuning("buffer_dead_va_limit")
 
 // Descriptors are read-only for the whole launch: read them through the constant address space so
 // the uniform-index loads become scalar loads (s_load_*) into SGPRs instead of per-lane vector loads.

@@ -575,7 +575,9 @@ RTPB_HD bool table_has_key(const DevMaterial<T>& m, T wl, TablePtr table) {
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
 // iden: optional make_rcp of the denominator d.nrm, shared by several planes with the same normal.
 // AXN: the normal is (+0, +0, 1); AXC: cx and cy are +0 (axdot / axsub).
-template <bool AXN = false, bool AXC = false, typename T, class G = GuardBranch>
+// PH = false (positions only, the spot sweep's kPosOnly mode): the phase is not accumulated -- nothing the
+// position, the direction or the row's kill depends on reads it.
+template <bool AXN = false, bool AXC = false, bool PH = true, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
                         const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr, G* g = nullptr) {
     const T num = -axdot<AXN>(axsub<AXC>(r.x, cx), axsub<AXC>(r.y, cy), r.z - cz, nx, ny, nz);
@@ -588,10 +590,15 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
     o.y = r.y + vy;
     o.z = r.z + vz;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
-    const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
-    // dist * s * 2 * pi (RT:297): s = +-1 is a sign, and 2 * pi is exact, so ((d s) 2) pi == (+-d) (2 pi)
-    // bit for bit -- the two real products are the same number (overflow to inf included)
-    o.ph = r.ph + div1_as<T, G, true>((s < T(0) ? -dist : dist) * T(Const<T>::two_pi), r.wl, iwl, g) * n;
+    if constexpr (PH) {
+        const T dist = tsqrt<T>(vx * vx + vy * vy + vz * vz, g);
+        // dist * s * 2 * pi (RT:297): s = +-1 is a sign, and 2 * pi is exact, so ((d s) 2) pi == (+-d) (2 pi)
+        // bit for bit -- the two real products are the same number (overflow to inf included)
+        o.ph = r.ph + div1_as<T, G, true>((s < T(0) ? -dist : dist) * T(Const<T>::two_pi), r.wl, iwl, g) * n;
+    } else {
+        (void)n; (void)iwl;
+        o.ph = r.ph;
+    }
     o.wl = r.wl;
     kill_if(exclude_backward && s == T(-1), o);
     if (t_out) *t_out = t;
@@ -622,8 +629,8 @@ RTPB_HD T sphere_root(T B, T root) {
 }
 
 // rxy (AX only): x x + y y of the ray's position, as on_sphere computed it at the previous axial surface (the
-// same expression for a center on the axis) -- or nullptr
-template <bool AX = false, typename T, class G = GuardBranch>
+// same expression for a center on the axis) -- or nullptr.  PH = false: positions only (see to_plane).
+template <bool AX = false, bool PH = true, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr,
                           const T* rxy = nullptr) {
     const T ox = axsub<AX>(r.x, s.c[0]), oy = axsub<AX>(r.y, s.c[1]), oz = r.z - s.c[2];
@@ -635,9 +642,14 @@ RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rc
     o.y = r.y + r.dy * t;
     o.z = r.z + r.dz * t;
     o.dx = r.dx; o.dy = r.dy; o.dz = r.dz;
-    const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
-    const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz, g);
-    o.ph = r.ph + div1_as<T, G, true>(dist * T(Const<T>::two_pi), r.wl, iwl, g) * n;  // == (d 2) pi, see to_plane
+    if constexpr (PH) {
+        const T sx = o.x - r.x, sy = o.y - r.y, sz = o.z - r.z;
+        const T dist = tsqrt<T>(sx * sx + sy * sy + sz * sz, g);
+        o.ph = r.ph + div1_as<T, G, true>(dist * T(Const<T>::two_pi), r.wl, iwl, g) * n;  // == (d 2) pi, see to_plane
+    } else {
+        (void)n; (void)iwl;
+        o.ph = r.ph;
+    }
     o.wl = r.wl;
     return o;
 }
@@ -851,15 +863,15 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s, T* rxy_out = nul
 // The "at" plane (the lens plane, RT:1790-1793) is emitted first: it depends on r only.
 // UNI: the media on both sides are uniform (Constant, or Vacuum with an ordinary wavelength on every lane of the
 // wave): F, B, n1 f and n1 n1 f + n2 n2 f come from the descriptor, computed on the host by the same operations.
-template <typename T, bool AX, bool UNI, typename EmitAt, class G>
+template <typename T, bool AX, bool UNI, bool PH, typename EmitAt, class G>
 RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                        Ray<T>& after, G* g) {
     const T f = s.f;
     const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
     // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
     const Rcp<T> iden = make_rcp(axdot<AX>(r.dx, r.dy, r.dz, nx, ny, nz));
-    emit_at(to_plane<AX, AX>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
-                             g));   // RT:1790-1793
+    emit_at(to_plane<AX, AX, PH>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr),
+                                 &iden, g));   // RT:1790-1793
     T Fx, Fy, Fz, Bx, By, Bz;
     if constexpr (UNI) {
         Fx = s.lF[0]; Fy = s.lF[1]; Fz = s.lF[2];
@@ -870,7 +882,8 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     }
     // axial and uniform: F = (+0, +0, Fz), so the front focal plane has the axial center form too
     constexpr bool AXF = AX && UNI;
-    const Ray<T> rf = to_plane<AX, AXF>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
+    const Ray<T> rf = to_plane<AX, AXF, PH>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden,
+                                            g);
     const T dn = axdot<AX>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
     T spx, spy, spz;
     if constexpr (AX) {
@@ -944,12 +957,16 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     }
     o.wl = r.wl;
     kill_if(tabs<T>(sin_t1) > s.sin_a || tabs<T>(sin_t2) > s.sin_a, o);
-    const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
-    // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
-    const T k = iwl.k;
-    o.ph = rf.ph - k * n1 * pw + k * (UNI ? s.lph : n1 * n1 * f + n2 * n2 * f);
-    after = to_plane<AX, AX>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
-                             static_cast<const Rcp<T>*>(nullptr), g);
+    if constexpr (PH) {
+        const T pw = r1x * rf.dx + r1y * rf.dy + r1z * rf.dz;
+        // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
+        const T k = iwl.k;
+        o.ph = rf.ph - k * n1 * pw + k * (UNI ? s.lph : n1 * n1 * f + n2 * n2 * f);
+    } else {
+        o.ph = rf.ph;
+    }
+    after = to_plane<AX, AX, PH>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
+                                 static_cast<const Rcp<T>*>(nullptr), g);
 }
 
 // The front-side test d . input_axis < 0 (RT:1187-1192).  POS_ONLY (the sweep's final-position semantics) on an
@@ -974,7 +991,9 @@ RTPB_HD bool front_side_fails(const Ray<T>& r, const DevSurface<T>& s) {
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
 // AX: the surface has kAxial geometry (not for PLANE_MIRROR).
-// MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell).
+// MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell) and
+// positions only: the phase is not accumulated (a spot diagram reads x, y, z; no position, direction or kill depends
+// on the phase), so the phase column of `after` is r's.
 // rxy (kAxial spheres in kPosOnly runs): in: x x + y y of r (on_sphere's value at the previous axial surface); out:
 // the same of the intersection point, for the next one.
 constexpr int kPosOnly = 1;
@@ -982,20 +1001,21 @@ template <typename T, int KIND, bool AX = false, int MODE = 0, typename EmitAt, 
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                           Ray<T>& after, G* g = nullptr, T* rxy = nullptr) {
     constexpr bool kTirFill = (MODE & kPosOnly) == 0;
+    constexpr bool kPhase = (MODE & kPosOnly) == 0;
     if constexpr (KIND == PERFECT_LENS) {
         // uniform media: the instantiation with the focal points and constants in scalar registers (a wave-uniform
         // branch between two whole steps: merged values would cost vector registers on both paths)
         if (s.rcp_ok & kLensUni) {
             RTPB_NO_SPECULATE();
-            lens_step<T, AX, true>(s, r, n1, n2, iwl, emit_at, after, g);
+            lens_step<T, AX, true, kPhase>(s, r, n1, n2, iwl, emit_at, after, g);
         } else {
-            lens_step<T, AX, false>(s, r, n1, n2, iwl, emit_at, after, g);
+            lens_step<T, AX, false, kPhase>(s, r, n1, n2, iwl, emit_at, after, g);
         }
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
         if constexpr (KIND == SPHERE) {
-            ri = sphere_hit<AX>(r, s, n1, iwl, g, static_cast<const T*>(rxy));
+            ri = sphere_hit<AX, kPhase>(r, s, n1, iwl, g, static_cast<const T*>(rxy));
             Nx = axsub<AX>(ri.x, s.c[0]);                                  // (p - c) / R, RT:1476
             Ny = axsub<AX>(ri.y, s.c[1]);
             Nz = ri.z - s.c[2];
@@ -1020,8 +1040,8 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             }
         } else {                                                           // FLAT, PLANE_MIRROR
             Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-            ri = to_plane<AX, AX>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
-                                  static_cast<const Rcp<T>*>(nullptr), g);          // RT:1331-1337, 1398-1403
+            ri = to_plane<AX, AX, kPhase>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
+                                          static_cast<const Rcp<T>*>(nullptr), g);  // RT:1331-1337, 1398-1403
         }
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);

@@ -357,6 +357,7 @@ int rtpb_set_tuning(const char* key, int64_t value) {
         return RTPB_OK;
     }
     if (std::strcmp(key, "buffer_pool_buffers") == 0) return set_buffer_pool_keep(value);
+    if (std::strcmp(key, "buffer_dead_va_limit") == 0) return set_buffer_dead_va_limit(value);
     return fail(RTPB_E_INVALID, std::string("unknown tuning key ") + key);
 }
 

@@ -65,10 +65,13 @@ class HistoryWriter:
             if item is None:
                 return
             index, arr, event, buf, src = item
+            item = None
             try:
                 if event is not None:
                     event.synchronize()
-                del src             # the device history may be freed (and its memory reused) from here on
+                # the copy has finished: drop the last references to the device history, so its memory may be
+                # freed (and reused by the next trace) while this chunk goes to disk
+                del src
                 tmp = self._chunk_file(index) + ".tmp"
                 with open(tmp, "wb") as f:
                     f.write(memoryview(np.ascontiguousarray(arr)).cast("B"))

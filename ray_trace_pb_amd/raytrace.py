@@ -54,8 +54,11 @@ def get_ray_fan(pt, theta_max: float, n_thetas: int, wavelengths, nphis: int = 1
     cos(theta) c + cos(phi) sin(theta) ex + sin(phi) sin(theta) ey with ex = y x c / |.|, ey = c x ex,
     theta in linspace(-theta_max, theta_max, n_thetas), phi = k 2 pi / nphis.  Phase 0.
 
+    ``wavelengths``: one value, or one per ray (an array of n_thetas*nphis values, NumPy or torch), as
+    ``rays[:, 7] = wavelengths`` assigns it (RT:94).
+
     With ``device`` (a torch CUDA device), the fan is generated directly in HBM by the ``rtpb_ray_fan_tables``
-    kernel and returned as a torch tensor (``wavelengths`` must then be a scalar).  With ``devices`` (GPU
+    kernel (``rtpb_ray_fan_tables_wl`` for per-ray wavelengths) and returned as a torch tensor.  With ``devices`` (GPU
     indices) it is generated as contiguous ray-index shards, one per GPU (whole phi rows, as even as the
     row count allows), and returned as the list of per-device tensors -- the input of a multi-GPU
     ``System.ray_trace`` that never gathers (e.g. the C4 configuration, 100M rays over 8 GPUs)."""
@@ -65,6 +68,8 @@ def get_ray_fan(pt, theta_max: float, n_thetas: int, wavelengths, nphis: int = 1
     if devices is not None:
         import torch
         out = []
+        if not _is_torch_cuda(wavelengths) and np.ndim(wavelengths) > 0 and np.size(wavelengths) > 1:
+            wavelengths = _wavelength_column(wavelengths, int(n_thetas) * int(nphis))   # host column, once
         for (p0, p1), d in zip(shard_bounds(int(nphis), len(devices)), devices):
             buf = torch.empty(((p1 - p0) * n_thetas, 8), device=torch.device("cuda", int(d)),
                               dtype=torch.float32 if dtype in ("float32", np.float32, torch.float32) else torch.float64)
@@ -113,11 +118,48 @@ def _fan_tables(theta_max, n_thetas, nphis, center_ray, center_dtype):
     return enx, eny, tcs, pcs
 
 
+def _wavelength_column(wavelengths, n, device=None):
+    """``rays[:, 7] = wavelengths`` for n rays (RT:94, RT:159) as a float64 column: None for one wavelength
+    (a scalar or a one-element array: the kernel's constant), else the n per-ray values -- NumPy (host) or, for
+    a torch tensor or with ``device``, a contiguous CUDA tensor.  Shapes NumPy's assignment rejects raise."""
+    import torch
+    if isinstance(wavelengths, torch.Tensor):
+        if wavelengths.numel() == 1:
+            return None
+        dev = device if device is not None else (wavelengths.device if wavelengths.is_cuda else None)
+        col = torch.empty(n, dtype=torch.float64, device=dev if dev is not None else "cpu")
+        col[:] = wavelengths.to(device=col.device, dtype=torch.float64)
+        return col
+    w = np.asarray(wavelengths)
+    if w.ndim == 0 or w.size == 1:
+        return None
+    if w.shape == (n,) and w.dtype == np.float64 and w.flags.c_contiguous:
+        col = w
+    else:
+        col = np.empty(n)
+        col[:] = w                       # the reference's assignment: same broadcasting, same errors
+    if device is not None:
+        return torch.from_numpy(col).to(device)
+    return col
+
+
+def _wavelength_args(wavelength, n_total, lo, hi, device):
+    """(scalar wavelength, per-ray CUDA column of rays lo..hi or None) for a generator launch."""
+    col = _wavelength_column(wavelength, n_total)
+    if col is None:
+        return float(np.asarray(wavelength.cpu() if hasattr(wavelength, "cpu") else wavelength).ravel()[0]), None
+    import torch
+    part = col[lo:hi]
+    part = part.to(device) if isinstance(part, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(part)).to(device)
+    return 0.0, part.contiguous()
+
+
 def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0, 1), phi_rows=None):
     """Write get_ray_fan(pt, theta_max, n_thetas, wavelength, nphis, center_ray) into the torch CUDA
     buffer ``buf`` ((n_thetas*nphis, 8), float64 or float32) on its current stream.  ``phi_rows=(p0, p1)``
     writes only rays p0*n_thetas .. p1*n_thetas - 1 (a contiguous shard; ``buf`` then has
-    (p1-p0)*n_thetas rows).
+    (p1-p0)*n_thetas rows).  ``wavelength``: a scalar or the whole fan's n_thetas*nphis per-ray values
+    (NumPy or torch; a shard reads its own slice).
 
     Every host-side value of RT:71-81 -- the linspace thetas, the phis, their np.cos / np.sin, and the
     enx / eny basis -- is evaluated here with NumPy exactly as the reference does (n_thetas + nphis
@@ -135,10 +177,19 @@ def fan_into(buf, pt, theta_max, n_thetas, wavelength, nphis=1, center_ray=(0, 0
     if p1 == p0:
         return buf
     pcs = np.ascontiguousarray(pcs[p0:p1])
-    C.check(C.lib().rtpb_ray_fan_tables(buf.device.index or 0, code, buf.data_ptr(), vec[0].ctypes.data,
-                                        int(n_thetas), p1 - p0, vec[1].ctypes.data, vec[2].ctypes.data,
-                                        vec[3].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, float(wavelength),
-                                        torch.cuda.current_stream(buf.device).cuda_stream))
+    nt = int(n_thetas)
+    wl, col = _wavelength_args(wavelength, nt * int(nphis), p0 * nt, p1 * nt, buf.device)
+    stream = torch.cuda.current_stream(buf.device).cuda_stream
+    if col is None:
+        C.check(C.lib().rtpb_ray_fan_tables(buf.device.index or 0, code, buf.data_ptr(), vec[0].ctypes.data,
+                                            nt, p1 - p0, vec[1].ctypes.data, vec[2].ctypes.data,
+                                            vec[3].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, wl, stream))
+    else:
+        # col is read by the kernel on this stream; torch's allocator reuses its memory only in stream order
+        C.check(C.lib().rtpb_ray_fan_tables_wl(buf.device.index or 0, code, buf.data_ptr(), vec[0].ctypes.data,
+                                               nt, p1 - p0, vec[1].ctypes.data, vec[2].ctypes.data,
+                                               vec[3].ctypes.data, tcs.ctypes.data, pcs.ctypes.data, col.data_ptr(),
+                                               stream))
     return buf
 
 
@@ -148,7 +199,9 @@ def get_collimated_rays(pt, displacement_max, n_disps: int, wavelengths, nphis: 
 
     index = idisp*nphis + iphi; position pt + off (n1 cos phi + n2 sin phi) with n1 = y x normal
     (or normal x x when normal is along y), n2 = normal x n1; offsets linspace(-dmax, dmax, n_disps).
-    With ``device`` the bundle is generated in HBM by ``rtpb_collimated_rays_tables`` (scalar wavelength)."""
+    ``wavelengths``: one value or one per ray (n_disps*nphis), "either floating point or an array the same size
+    as n_disps * nphis" (RT:115).  With ``device`` the bundle is generated in HBM by
+    ``rtpb_collimated_rays_tables`` (``rtpb_collimated_rays_tables_wl`` for per-ray wavelengths)."""
     if np.abs(np.linalg.norm(normal) - 1) > 1e-12:
         raise ValueError("normal must be a normalized vector")
     if device is not None:
@@ -192,11 +245,19 @@ def _collimated_device(pt, displacement_max, n_disps, wavelength, nphis, phi_sta
     n2 = n2 / np.linalg.norm(n2)
     pcs = np.ascontiguousarray(np.stack((np.cos(phis), np.sin(phis)), axis=1), dtype=np.float64)
     vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (pt, normal, n1, n2)]
-    C.check(C.lib().rtpb_collimated_rays_tables(dev.index or 0, C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32,
-                                                out.data_ptr(), vec[0].ctypes.data, int(n_disps), int(nphis),
-                                                vec[1].ctypes.data, vec[2].ctypes.data, vec[3].ctypes.data,
-                                                offs.ctypes.data, pcs.ctypes.data, float(wavelength),
-                                                torch.cuda.current_stream(dev).cuda_stream))
+    n = int(n_disps) * int(nphis)
+    wl, col = _wavelength_args(wavelength, n, 0, n, dev)
+    code = C.RTPB_F64 if tdt == torch.float64 else C.RTPB_F32
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    if col is None:
+        C.check(C.lib().rtpb_collimated_rays_tables(dev.index or 0, code, out.data_ptr(), vec[0].ctypes.data,
+                                                    int(n_disps), int(nphis), vec[1].ctypes.data, vec[2].ctypes.data,
+                                                    vec[3].ctypes.data, offs.ctypes.data, pcs.ctypes.data, wl, stream))
+    else:
+        C.check(C.lib().rtpb_collimated_rays_tables_wl(dev.index or 0, code, out.data_ptr(), vec[0].ctypes.data,
+                                                       int(n_disps), int(nphis), vec[1].ctypes.data,
+                                                       vec[2].ctypes.data, vec[3].ctypes.data, offs.ctypes.data,
+                                                       pcs.ctypes.data, col.data_ptr(), stream))
     return out
 
 

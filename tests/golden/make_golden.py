@@ -3,6 +3,7 @@
 Run from anywhere inside this container (not on the GPU box -- /root/reference does not exist there):
 
     python tests/golden/make_golden.py [name,...]     # only the named recipes (no paraxial/generator files)
+    python tests/golden/make_golden.py generators     # only generators.npz
 
 The script re-launches itself in a child interpreter whose ``sys.path`` holds only
 /root/reference/src (the reference's ``raytrace`` package) and this directory, with cwd=/tmp, so the
@@ -34,6 +35,9 @@ def _child():
     meta = {"numpy": np.__version__, "reference": "QI2lab/ray_trace_pb @ 2024_10_08"}
 
     only = [v for v in os.environ.get("RTPB_GOLDEN_ONLY", "").split(",") if v]
+    if only == ["generators"]:
+        _generators(np, rt, systems)
+        return
     # float32 INPUT variants (<recipe>_f32in): the reference run on the recipe's rays rounded to
     # float32, i.e. what a caller handing it float32 arrays gets back (a float64 history)
     recipes = [(n, r, False) for n, r in systems.RECIPES.items()]
@@ -89,7 +93,11 @@ def _child():
     with open(os.path.join(HERE, "paraxial.json"), "w") as f:
         json.dump(par, f, indent=1)
 
-    # ray generators and analysis utilities (RT:45-353)
+    _generators(np, rt, systems)
+
+
+def _generators(np, rt, systems):
+    """Ray generators and analysis utilities (RT:45-353) -> generators.npz."""
     gens = {
         "fan": rt.get_ray_fan([1., 2., 3.], 0.3, 7, 0.5, nphis=5, center_ray=(0, 0, 1)),
         "fan_tilted": rt.get_ray_fan([0., 0., 0.], 0.2, 5, 0.6, nphis=3,
@@ -109,6 +117,22 @@ def _child():
     gens["angle_out"], gens["angle_na"] = ang, na
     dists, near = rt.dist_pt2plane(r1[:, :3], np.array([0., 0.6, 0.8]), np.array([1., 2., 3.]))
     gens["dist_out"], gens["dist_near"] = dists, near
+    # per-ray wavelengths: "either floating point or an array the same size as n_disps * nphis" (RT:115; the
+    # fan's RT:94 is the same assignment); the arrays are stored beside the bundles as <case>_wl
+    wl_cases = {
+        "fan_wl": ("fan", ([1., 2., 3.], 0.3, 7, np.linspace(0.4, 0.8, 35)), {"nphis": 5}),
+        "fan_wl3": ("fan", ([0., 0., -5.], 0.02, 11, np.tile([0.7065, 0.855, 1.015], 44)), {"nphis": 12}),
+        "fan_wl1": ("fan", ([0., 0., 0.], 0.2, 5, np.array([0.55])), {"nphis": 3,
+                                                                       "center_ray": tuple(systems.unit([0.6, 0, 0.8]))}),
+        "coll_wl": ("coll", ([0., 1., -2.], 3., 5, np.linspace(0.45, 0.65, 20, dtype=np.float32)),
+                    {"nphis": 4, "phi_start": 0.3}),
+        "coll_wl_tilted": ("coll", ([0., 0., 0.], 2., 4, np.repeat([0.405, 0.785], 6)),
+                           {"nphis": 3, "normal": [np.sin(0.2), 0, np.cos(0.2)]}),
+    }
+    for name, (kind, args, kw) in wl_cases.items():
+        fn = rt.get_ray_fan if kind == "fan" else rt.get_collimated_rays
+        gens[name] = fn(*args, **kw)
+        gens[name + "_wl"] = np.asarray(args[3])
     np.savez_compressed(os.path.join(HERE, "generators.npz"), **gens)
 
 

@@ -98,3 +98,20 @@ def fastdiv_check(a, a2, a3, b, kill):
     rc = _fastdiv.fastdiv_check(*[x.ctypes.data for x in arrs], k.ctypes.data, n, out.ctypes.data)
     assert rc == 0, rc
     return out
+
+
+VMM_SRC = os.path.join(HERE, "native", "vmm_remap_check.hip")
+VMM_OUT = os.path.join(HERE, "native", "_build", "vmm_remap_check")
+
+
+def build_vmm_check():
+    """hipcc (gfx950) build of the torch-free HIP virtual-memory remapping check (an executable; run by
+    tests/test_gpu_vmm.py and tools/gpu_run.sh vmm)."""
+    if os.path.exists(VMM_OUT) and os.path.getmtime(VMM_OUT) >= os.path.getmtime(VMM_SRC):
+        return VMM_OUT
+    os.makedirs(os.path.dirname(VMM_OUT), exist_ok=True)
+    tmp = f"{VMM_OUT}.{os.getpid()}.tmp"
+    subprocess.run([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--offload-arch=gfx950", "-O2", "-std=c++17",
+                    "-Wall", "-o", tmp, VMM_SRC], check=True)
+    os.replace(tmp, VMM_OUT)
+    return VMM_OUT

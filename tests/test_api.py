@@ -234,3 +234,27 @@ def test_plan_cache_never_frees_a_plan_in_use(monkeypatch):
     assert destroyed == [pa.value]           # freed by its last user
     E.plan_for(Low("d"))                     # evicts "b" (unused): freed at once
     assert len(destroyed) == 2
+
+
+def test_host_generators_per_ray_wavelengths_match_reference_fixtures():
+    """The host generators with one wavelength per ray (RT:94, RT:159) against the reference's output."""
+    import os
+    from parity import GOLDEN, same_bits
+    import systems
+    d = np.load(os.path.join(GOLDEN, "generators.npz"))
+    assert same_bits(rt.get_ray_fan([1., 2., 3.], 0.3, 7, d["fan_wl_wl"], nphis=5), d["fan_wl"])
+    assert same_bits(rt.get_ray_fan([0., 0., -5.], 0.02, 11, d["fan_wl3_wl"], nphis=12), d["fan_wl3"])
+    assert same_bits(rt.get_ray_fan([0., 0., 0.], 0.2, 5, d["fan_wl1_wl"], nphis=3,
+                                    center_ray=tuple(systems.unit([0.6, 0, 0.8]))), d["fan_wl1"])
+    assert same_bits(rt.get_collimated_rays([0., 1., -2.], 3., 5, d["coll_wl_wl"], nphis=4, phi_start=0.3),
+                     d["coll_wl"])
+    assert same_bits(rt.get_collimated_rays([0., 0., 0.], 2., 4, d["coll_wl_tilted_wl"], nphis=3,
+                                            normal=[np.sin(0.2), 0, np.cos(0.2)]), d["coll_wl_tilted"])
+
+
+def test_wavelength_column_follows_numpy_assignment():
+    col = rt._wavelength_column(np.float32([0.5, 0.6, 0.7]), 3)
+    assert col.dtype == np.float64 and np.array_equal(col, np.float32([0.5, 0.6, 0.7]).astype(np.float64))
+    assert rt._wavelength_column(0.5, 10) is None and rt._wavelength_column(np.array([0.5]), 10) is None
+    with pytest.raises(ValueError):
+        rt._wavelength_column(np.ones(4), 3)

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "rtpb.h")
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|double|const char\s*\*)\s*(rtpb_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|double|const char\s*\*|void\s*\*?)\s*(rtpb_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol():

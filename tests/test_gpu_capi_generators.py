@@ -94,3 +94,44 @@ def test_device_generators_bitwise_vs_reference_fixtures(name):
     if kind == "fan":
         shards = gen(*args, **kw, devices=[0, 0, 0])
         assert np.array_equal(torch.cat([s.cpu() for s in shards]).numpy(), ref)
+
+
+WL_CASES = {   # tests/golden/make_golden.py: per-ray wavelengths (RT:94, RT:115, RT:159); <name>_wl holds the array
+    "fan_wl": ("fan", ([1., 2., 3.], 0.3, 7), dict(nphis=5)),
+    "fan_wl3": ("fan", ([0., 0., -5.], 0.02, 11), dict(nphis=12)),
+    "fan_wl1": ("fan", ([0., 0., 0.], 0.2, 5), dict(nphis=3, center_ray=tuple(systems.unit([0.6, 0, 0.8])))),
+    "coll_wl": ("coll", ([0., 1., -2.], 3., 5), dict(nphis=4, phi_start=0.3)),
+    "coll_wl_tilted": ("coll", ([0., 0., 0.], 2., 4), dict(nphis=3, normal=[np.sin(0.2), 0, np.cos(0.2)])),
+}
+
+
+@pytest.mark.parametrize("name", list(WL_CASES))
+@pytest.mark.parametrize("wl_kind", ["numpy", "torch"])
+def test_device_generators_per_ray_wavelengths_bitwise(name, wl_kind):
+    """get_ray_fan / get_collimated_rays with one wavelength per ray (rtpb_*_tables_wl) against the
+    reference's own output on the same arrays (generators.npz): float64 bit for bit, float32 storage = the
+    fixture rounded once; the host generator gives the same bits; fans also as per-device phi-row shards."""
+    import os
+    from parity import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "generators.npz"))
+    ref, wls = d[name], d[name + "_wl"]
+    kind, args, kw = WL_CASES[name]
+    gen = rt.get_ray_fan if kind == "fan" else rt.get_collimated_rays
+    w = wls if wl_kind == "numpy" else torch.from_numpy(wls).to(DEV)
+    got = gen(*args, w, **kw, device=DEV)
+    assert got.dtype == torch.float64 and same_bits(got.cpu().numpy(), ref)
+    got32 = gen(*args, w, **kw, device=DEV, dtype="float32")
+    assert same_bits(got32.cpu().numpy(), ref.astype(np.float32))
+    assert same_bits(gen(*args, wls, **kw), ref)                       # the host generator
+    if kind == "fan":
+        for devs in ([0, 0, 0], [0, 0]):
+            shards = gen(*args, w, **kw, devices=devs)
+            assert same_bits(torch.cat([s.cpu() for s in shards]).numpy(), ref)
+
+
+def test_device_generators_reject_what_numpy_rejects():
+    """A per-ray wavelength array of the wrong length fails as the reference's assignment does."""
+    with pytest.raises(ValueError):
+        rt.get_ray_fan([0., 0., 0.], 0.1, 5, np.ones(7), nphis=2, device=DEV)
+    with pytest.raises((ValueError, RuntimeError)):
+        rt.get_collimated_rays([0., 0., 0.], 1., 3, torch.ones(5, device=DEV), nphis=2, device=DEV)

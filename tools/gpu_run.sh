@@ -18,6 +18,7 @@
 #   pmc_c5           PMC passes of the fused C5 sweep kernel (1 field)
 #   e2e              host phases of the drop-in call (tools/e2e_phases.py)
 #   power            socket power / clock under the history kernels (tools/power_probe.py)
+#   vmm              tests/native/vmm_remap_check (HIP virtual-memory remapping, no torch; built in-tree)
 #   valu             issue cost of the kernels' VALU instructions (tools/valu/valu_rates.hip, built in-tree)
 #   ab:LIB[,LIB..]   A/B of the in-tree library against experiment builds (tools/ab_variants.py, histories;
 #                    C5 sweep per library, the in-tree one before and after)
@@ -58,6 +59,7 @@ for s in "$@"; do
     pmc_c5) step pmc_c5 900 bash tools/pmc_kernel.sh "$P/pmc_c5" sweep_kernel python3 tools/c5_sweep.py --fields 1 --warmup 0 ;;
     e2e) step e2e 600 python3 tools/e2e_phases.py ;;
     valu) step valu 300 tools/valu/_build/valu_rates ;;
+    vmm) step vmm 300 tests/native/_build/vmm_remap_check 10 ;;
     power)
       for args in "--config c4:1.0 --planes all" "--config c4:1.0 --planes final" "--config c3:1.0 --planes all" \
                   "--config c3:1.0 --planes final"; do
