@@ -260,9 +260,9 @@ class Workload:
         table keys, output allocation and the launch (ms per call, synchronised)."""
         import torch
         dt = "float32" if self.code != self._E.C.RTPB_F64 else None
-        # System.ray_trace allocates its own history: a history of >= 1 GiB is a history buffer, and the
-        # library's pool hands a repeated call the buffer the previous history freed -- first the timed loop's
-        # own buffer, then the same one call after call (stream-ordered reuse on the launch stream)
+        # System.ray_trace allocates its own history: a history of >= 512 MiB comes from the history pool, whose
+        # caching allocator hands a repeated call the block the previous history freed -- first the timed loop's
+        # own buffer, then the same one call after call (torch's stream-ordered reuse on the launch stream)
         del self.out
         h = self.system.ray_trace(self.rays, self.m0, self.m1, dtype=dt)
         del h
@@ -781,17 +781,19 @@ def main():
             line["e2e_note"] = ("System.ray_trace(torch rays, Vacuum(), Vacuum(), dtype='float32') on the device-"
                                 "resident C3 bundle, the median of 15 calls: lowering (memoised by content), "
                                 "Ebaf11 table keys (the previous bundle's, checked by the kernel's table-miss "
-                                "flag), history allocation (a pooled history buffer: the timed loop's own, "
-                                "reused), launch, miss-flag read, synchronise. e2e_kernel_ms: the same call's "
+                                "flag), history allocation (the history pool, torch's caching allocator: the timed "
+                                "loop's block, reused), launch, miss-flag read, synchronise. e2e_kernel_ms: the same call's "
                                 "kernel (HIP events); e2e_overhead_ms: the host-side cost of the drop-in call "
                                 "(tools/e2e_phases.py splits it by phase)")
         if alt_ms is not None:
             line["placement_check"] = {
                 "kernel_ms_history_buffer": kernel_ms, "kernel_ms_torch_empty": alt_ms,
-                "note": "value: the trace into raytrace.history_buffer (rtpb_buffer_alloc: physical chunks mapped "
-                        "in shuffled order, the product's out= buffer for repeated traces); kernel_ms_torch_empty: "
-                        "the same launches into a torch.empty history (the default allocation of System.ray_trace "
-                        "without out=), whose many-plane write rate depends on where it lands (DESIGN.md 5)"}
+                "note": "value: the trace into raytrace.history_buffer (a tensor of the history pool: torch's caching "
+                        "allocator over librtpb's shuffled 64 MiB chunk mappings, the default allocation of "
+                        "System.ray_trace for histories of POOLED_HISTORY_BYTES = 512 MiB or more); "
+                        "kernel_ms_torch_empty: the same launches into a torch.empty history (torch's default pool, "
+                        "System.ray_trace's allocation below 512 MiB), whose many-plane write rate depends on where "
+                        "it lands (DESIGN.md 5)"}
         line["per_rank"] = per_rank
         line["distinct_gpus"] = len({(p["pci"], p["uuid"]) for p in per_rank})
         if line["distinct_gpus"] < world:

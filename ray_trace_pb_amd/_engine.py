@@ -454,16 +454,17 @@ def _capsule_api():
 
 
 def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
-    """A C-contiguous torch CUDA tensor of ``shape`` and ``dtype`` (float32 / float64) on ``device`` whose
-    memory comes from rtpb_buffer_alloc: physical chunks (64 MiB) mapped in a shuffled order, so a history
-    traced into it writes at the fast rate whatever the physical state of the card (a history's many-plane
-    write pattern runs 15-45 % slower into physically contiguous placements).
+    """A C-contiguous torch CUDA tensor of ``shape`` and ``dtype`` (float32 / float64) on ``device`` whose device
+    memory is mapped in shuffled 64 MiB chunks, so a history traced into it writes at the fast rate whatever the
+    physical state of the card (a history's many-plane write pattern runs 15-45 % slower into physically
+    contiguous placements).
 
-    Stream semantics are those of torch's caching allocator: the buffer is allocated for ``stream`` (default:
-    the device's current stream); a use on another stream must be recorded with :func:`record_stream`
-    (torch's own ``Tensor.record_stream`` does nothing for this memory).  Freeing never blocks: the buffer
-    returns to the library's pool (the newest freed buffer per device is kept mapped), and the next buffer
-    of the same size makes its stream wait for every recorded use of the previous owner."""
+    Default (``chunk_bytes`` = 0): allocated by torch's caching allocator in the device's history pool
+    (:func:`history_pool`, ABI 7) for ``stream`` (default: the current stream) -- an ordinary torch tensor to
+    torch: ``Tensor.record_stream``, ``torch.cuda.memory_allocated`` and out-of-memory handling work as for any
+    other tensor.  ``chunk_bytes`` > 0 (placement studies): a library buffer of that chunk size
+    (rtpb_buffer_alloc, its own stream-ordered pool; a use on another stream is recorded with
+    :func:`record_stream`), exported through DLPack."""
     import torch
     if dtype not in (torch.float32, torch.float64):
         raise ValueError("history_buffer: dtype must be torch.float32 or torch.float64")
@@ -472,6 +473,10 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
         raise ValueError("history_buffer: a CUDA (HIP) device is required")
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     shape = tuple(int(v) for v in shape)
+    if not chunk_bytes:
+        if stream is not None and not isinstance(stream, torch.cuda.Stream):
+            stream = torch.cuda.ExternalStream(stream, device=torch.device("cuda", idx))
+        return pool_empty(shape, dtype, torch.device("cuda", idx), stream)
     elem = 8 if dtype == torch.float64 else 4
     nbytes = elem
     for v in shape:
@@ -487,6 +492,7 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
     if lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, seed, raw_stream, ctypes.byref(ptr), ctypes.byref(handle)):
         # the device may be full of blocks torch's caching allocator holds: release them and retry once
         torch.cuda.synchronize(idx)
+        trim_history_buffers()
         torch.cuda.empty_cache()
         C.check(lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, seed, raw_stream, ctypes.byref(ptr),
                                       ctypes.byref(handle)))
@@ -510,7 +516,7 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
 
 
 _POOLS = {}
-_ALLOCATORS = {}            # the pools hold a raw pointer to their allocator: keep it alive with the pool
+_ALLOCATORS = {}            # a MemPool holds a raw pointer to its allocator: allocators live as long as the process
 _pools_lock = threading.Lock()
 
 
@@ -519,17 +525,20 @@ def history_pool(device_index):
     librtpb's shuffled-chunk mappings as its segment allocator (rtpb_torch_alloc / rtpb_torch_free, ABI 7).
     torch owns everything else -- caching, stream-ordered reuse (Tensor.record_stream), memory statistics and
     out-of-memory handling; ``use_on_oom``: an allocation outside the pool that runs out of memory may take
-    the pool's cached blocks."""
+    the pool's cached blocks.  The pool's cached segments are released by :func:`trim_history_buffers` (a live
+    MemPool keeps them through torch.cuda.empty_cache())."""
     import torch
     idx = int(device_index)
     with _pools_lock:
         pool = _POOLS.get(idx)
         if pool is None:
-            C.lib()                 # loaded after torch: the allocator binds to torch's HIP runtime
-            alloc = torch.cuda.memory.CUDAPluggableAllocator(C.LIB_PATH, "rtpb_torch_alloc", "rtpb_torch_free")
+            alloc = _ALLOCATORS.get(idx)
+            if alloc is None:
+                C.lib()                 # loaded after torch: the allocator binds to torch's HIP runtime
+                alloc = _ALLOCATORS[idx] = torch.cuda.memory.CUDAPluggableAllocator(C.LIB_PATH, "rtpb_torch_alloc",
+                                                                                    "rtpb_torch_free")
             with torch.cuda.device(idx):
                 pool = torch.cuda.MemPool(alloc.allocator(), use_on_oom=True)
-            _ALLOCATORS[idx] = alloc
             _POOLS[idx] = pool
     return pool
 
@@ -558,10 +567,9 @@ def buffer_stats(device=-1):
 
 
 def record_stream(tensor, stream):
-    """``tensor.record_stream(stream)`` for every kind of device memory: torch's caching-allocator record,
-    plus the library's record when the tensor lies in a history buffer (rtpb_buffer_record_stream) -- torch
-    ignores memory it did not allocate, so a history_buffer (and any default System.ray_trace history of
-    POOLED_HISTORY_BYTES or more) used on a side stream must be recorded this way before it is freed."""
+    """``tensor.record_stream(stream)`` for every kind of device memory: torch's caching-allocator record
+    (history-pool tensors are torch allocations), plus the library's record when the tensor lies in a buffer of
+    the library's own pool (``history_buffer(..., chunk_bytes=...)``, rtpb_buffer_record_stream)."""
     tensor.record_stream(stream)
     if tensor.numel() == 0:
         return
@@ -572,22 +580,40 @@ def record_stream(tensor, stream):
 
 
 def history_buffers_held(device=-1):
-    """(bytes, buffers) the library's history-buffer pool holds on ``device`` (-1: every device): freed
-    buffers kept mapped for reuse, and retired ones whose last uses have not completed yet."""
+    """(bytes, segments) of history memory cached but not in use on ``device`` (-1: every device): free bytes of
+    the history pools' segments, plus freed buffers of the library's own pool (and retired ones whose last uses
+    have not completed yet)."""
     nb, cnt = ctypes.c_uint64(), ctypes.c_int32()
     C.check(C.lib().rtpb_buffer_held(int(device), ctypes.byref(nb), ctypes.byref(cnt)))
-    return int(nb.value), int(cnt.value)
+    held, n = int(nb.value), int(cnt.value)
+    with _pools_lock:
+        pools = list(_POOLS.items())
+    for idx, pool in pools:
+        if device >= 0 and idx != device:
+            continue
+        for seg in pool.snapshot():
+            free = int(seg["total_size"]) - int(seg["allocated_size"])
+            if free > 0:
+                held += free
+                n += 1
+    return held, n
 
 
 def trim_history_buffers():
-    """Release the device memory of every freed history_buffer (the library keeps the newest freed one per
-    device mapped for reuse; rtpb_buffer_trim waits for their last recorded uses)."""
+    """Release the device memory history buffers hold while unused: every history pool is dropped (torch then
+    returns its unused segments at once -- librtpb unmaps them -- and the rest when their tensors die; the next
+    history gets a new pool), and the library's own pool is emptied (rtpb_buffer_trim waits for the last
+    recorded uses)."""
+    with _pools_lock:
+        pools = list(_POOLS.values())
+        _POOLS.clear()
+    del pools
     C.check(C.lib().rtpb_buffer_trim())
 
 
 def device_empty(shape, dtype, device):
-    """torch.empty on a CUDA device; on an out-of-memory error the history-buffer pool (memory torch cannot
-    see) is released and the allocation retried once."""
+    """torch.empty on a CUDA device; on an out-of-memory error the cached history memory (the history pools'
+    unused segments, the library's own pool) is released and the allocation retried once."""
     import torch
     try:
         return torch.empty(shape, dtype=dtype, device=device)
@@ -622,8 +648,10 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
         out = device_empty(shape, tdt, rays.device)
     lo, hi = plane_mask(planes)
+    cur = None
     if stream is None:
-        stream = torch.cuda.current_stream(rays.device).cuda_stream
+        cur = torch.cuda.current_stream(rays.device)
+        stream = cur.cuda_stream
     lib = C.lib()
     with plan_ref(low) as plan:
         if miss is None:
@@ -633,9 +661,12 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
             C.check(lib.rtpb_trace_checked(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
                                            0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr()))
     if n:
-        # a history buffer (out=, or rays read from a previous history) used on this stream: recorded, so a
-        # later owner of the memory waits for this launch (a no-op for the allocation stream and for memory
-        # that is not a history buffer)
+        # the launch's use of `out` and of the rays on this stream, recorded: torch's allocator (a no-op on the
+        # tensor's own stream) and the library's own buffer pool then hand the memory to a later owner only after
+        # this launch
+        if cur is not None:
+            out.record_stream(cur)
+            rays.record_stream(cur)
         lib.rtpb_buffer_record_stream(out.data_ptr(), stream)
         lib.rtpb_buffer_record_stream(rays.data_ptr(), stream)
     return out

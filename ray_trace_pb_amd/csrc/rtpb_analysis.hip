@@ -3,6 +3,10 @@
 // and griddata-style interpolation of pupil phases onto a grid.
 #include "rtpb_internal.h"
 
+#include <algorithm>
+#include <array>
+#include <map>
+
 using namespace rtpbi;
 
 namespace {
@@ -113,6 +117,7 @@ struct SweepArgs {
     const double* __restrict__ grp;     // per group: x, y, z, wavelength
     const double* __restrict__ gn;      // FEAT bit 4: per group, n of the S+1 materials at its wavelength, then
                                         // per surface n_s / n_s+1, 1 / n_s+1 and host_rcp_ok(n_s+1) (0 / 1)
+    const int32_t* __restrict__ gidx;   // the groups of block row y: one (single) or two (PAIR) per row
     double* __restrict__ partials;
     int64_t n_thetas, nphis, gsize, tiles;
     double c[3], ex[3], ey[3];
@@ -122,10 +127,13 @@ struct SweepArgs {
 template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
 
-// kSweepRays rays per lane: block b covers tiles kSweepRays*b ... of its group; the rays go through each
-// surface in one straight-line region (one surface_step instantiation per ray, inside one run of equal surface
-// codes) so independent dependency chains interleave (two: -6 % vs one ray per lane); each tile is reduced
-// separately, with the same tree as spot_partial_kernel.
+// kSweepRays rays per lane, traced side by side: each surface runs one surface_step instantiation per ray in one
+// straight-line region (inside one run of equal surface codes), so independent dependency chains interleave (two:
+// -6 % vs one ray per lane); each ray's 256-ray tile is reduced separately, with the same tree as
+// spot_partial_kernel.  Single rows: block b covers tiles kSweepRays*b ... of one group.  PAIR rows (round 5): the
+// lane's two rays are the SAME ray of two groups of one field point -- the same fan at two wavelengths -- so the ray is
+// generated once, and a first refracting Flat / Sphere surface, where it is still the same ray for both, runs its
+// intersection, normal, tests and tangent basis once (surface_step_pair); only the refractions differ.
 #ifndef RTPB_SWEEP_RPL
 #define RTPB_SWEEP_RPL 2
 #endif
@@ -139,13 +147,17 @@ constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per b
 #define RTPB_SWEEP_WPE 6
 #endif
 #define RTPB_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(RTPB_SWEEP_WPE, 8)))
-template <typename TS, int FEAT>
+template <typename TS, int FEAT, bool PAIR>
 __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs a) {
+    static_assert(!PAIR || (kSweepRays == 2 && (FEAT & 16) != 0), "pairs: two rays per lane, host-evaluated media");
     __shared__ double red[kStats][kBlock];
-    const int64_t g = blockIdx.y;
-    const int64_t tile0 = kSweepRays * int64_t(blockIdx.x);
-    const double* gp = a.grp + 4 * g;
-    auto gen = [&](int64_t j) {
+    int64_t grp[kSweepRays], tile[kSweepRays];
+#pragma unroll
+    for (int q = 0; q < kSweepRays; ++q) {
+        grp[q] = PAIR ? a.gidx[2 * blockIdx.y + q] : a.gidx[blockIdx.y];
+        tile[q] = PAIR ? int64_t(blockIdx.x) : kSweepRays * int64_t(blockIdx.x) + q;
+    }
+    auto gen = [&](int64_t j, const double* gp) {
         const int64_t jj = j < a.gsize ? j : 0;
         const int64_t it = jj % a.n_thetas, ip = jj / a.n_thetas;
         const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
@@ -160,30 +172,81 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         return r;
     };
     Ray<double> r[kSweepRays];
+    if constexpr (PAIR) {
+        // the groups of a pair share the field point (the host pairs only such groups): one ray, two wavelengths
+        r[0] = gen(tile[0] * kBlock + threadIdx.x, a.grp + 4 * grp[0]);
+        r[1] = r[0];
+        r[1].wl = stored<TS>(a.grp[4 * grp[1] + 3]);
+    } else {
 #pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) r[q] = gen((tile0 + q) * kBlock + threadIdx.x);
+        for (int q = 0; q < kSweepRays; ++q) r[q] = gen(tile[q] * kBlock + threadIdx.x, a.grp + 4 * grp[q]);
+    }
     const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
     const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
     const cptr<double> table = (cptr<double>)(a.table);
-    const double wl0 = r[0].wl;                        // one wavelength per group
-    const Rcp<double> iwl = make_wl_rcp(wl0);          // shared divisor of every phase update, 2 pi / wl
-    // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the
-    // kernel's own material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
-    const cptr<double> gn = (cptr<double>)(a.gn) + g * (4 * a.nsurf + 1);
-    auto mat_n = [&](int k) -> double {
-        if constexpr ((FEAT & 16) != 0) return gn[k];
-        else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
+    // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the kernel's own
+    // material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
+    // single rows: every ray of the block has the group's wavelength, so the per-wavelength values of ray 0 serve all
+    Rcp<double> iwl[kSweepRays];
+    cptr<double> gn[kSweepRays];
+#pragma unroll
+    for (int q = 0; q < kSweepRays; ++q) {
+        iwl[q] = (PAIR || q == 0) ? make_wl_rcp(r[q].wl) : iwl[0];   // every phase update's divisor, 2 pi / wl
+        gn[q] = (cptr<double>)(a.gn) + grp[q] * (4 * a.nsurf + 1);
+    }
+    auto mat_n = [&](int q, int k) -> double {
+        if constexpr ((FEAT & 16) != 0) return gn[q][k];
+        else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), r[0].wl, table);
     };
-    double n_cur = mat_n(0);
+    // the surface's descriptor for ray q: with host-evaluated media, the Snell ratio and 1 / n2 of q's group (IEEE
+    // division on the host)
+    auto surface_for = [&](int q, int k, const DevSurface<double>& base) {
+        DevSurface<double> sd = base;
+        if constexpr ((FEAT & 16) != 0) {
+            sd.nr = gn[q][a.nsurf + 1 + k];
+            sd.rn2 = gn[q][2 * a.nsurf + 1 + k];
+            sd.rcp_ok = (sd.rcp_ok & ~(4 | 8)) | 4 | (gn[q][3 * a.nsurf + 1 + k] != 0.0 ? 8 : 0);
+        }
+        return sd;
+    };
+    double n_cur[kSweepRays];
+#pragma unroll
+    for (int q = 0; q < kSweepRays; ++q) n_cur[q] = (PAIR || q == 0) ? mat_n(q, 0) : n_cur[0];
     // runs of consecutive surfaces of one (kind, axial) code: each run loops inside one instantiation of the
     // surface step, so the rays' registers carry from surface to surface without the copies a per-surface
     // join of the kind branches needs (the ODT path of C5: 12 axial spheres, a lens, a flat = 3 runs)
     auto code_of = [&](int k) { return surface_code<double>((surf + k)->kind, (surf + k)->rcp_ok); };
+    constexpr int kMode = kPosOnly | ((FEAT & 16) != 0 ? kUniMedia : 0);
     // the statistics read only the final positions: the steps run with kPosOnly semantics (no TIR fill of the
     // position -- the next surface's intersection makes it NaN, and the final plane gets the rule below), and a run
     // of axial spheres carries x x + y y of each intersection point into the next sphere's quadratic
     double rxy[kSweepRays];
     int s = 0;
+    if constexpr (PAIR) {
+        // the first surface, shared by the pair when it refracts (Flat / Sphere)
+        const int code = a.nsurf > 0 ? code_of(0) : -1;
+        auto first = [&](auto kind, auto ax) {
+            constexpr int K = decltype(kind)::value;
+            constexpr bool A = decltype(ax)::value;
+            const DevSurface<double> base = load_surface<double>(surf);
+            const DevSurface<double> sd0 = surface_for(0, 0, base);
+            if constexpr (K == SPHERE && A) rxy[0] = r[0].x * r[0].x + r[0].y * r[0].y;
+            Ray<double> o0, o1;
+            surface_step_pair<double, K, A, kMode>(sd0, r[0], n_cur[0], iwl[0], sd0.nr, gn[1][a.nsurf + 1], r[1].wl, o0,
+                                                   o1, static_cast<GuardBranch*>(nullptr),
+                                                   K == SPHERE && A ? &rxy[0] : nullptr);
+            r[0] = o0;
+            r[1] = o1;
+#pragma unroll
+            for (int q = 0; q < kSweepRays; ++q) n_cur[q] = mat_n(q, 1);
+            s = 1;
+        };
+        using std::integral_constant;
+        if (code == 2 * SPHERE + 1) first(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
+        else if (code == 2 * SPHERE) first(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+        else if (code == 2 * FLAT + 1) first(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+        else if (code == 2 * FLAT) first(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+    }
     while (s < a.nsurf) {
         const int code = code_of(s);
         dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
@@ -195,28 +258,28 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
                 for (int q = 0; q < kSweepRays; ++q) rxy[q] = r[q].x * r[q].x + r[q].y * r[q].y;
             }
             do {
-                const double n_next = mat_n(s + 1);
-                DevSurface<double> sd = load_surface<double>(surf + s);
-                if constexpr ((FEAT & 16) != 0) {
-                    // the group's media are uniform: the Snell ratio and 1 / n2 from the host (IEEE division)
-                    sd.nr = gn[a.nsurf + 1 + s];
-                    sd.rn2 = gn[2 * a.nsurf + 1 + s];
-                    sd.rcp_ok = (sd.rcp_ok & ~(4 | 8)) | 4 | (gn[3 * a.nsurf + 1 + s] != 0.0 ? 8 : 0);
-                }
+                const DevSurface<double> base = load_surface<double>(surf + s);
+                double n_next[kSweepRays];
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q) n_next[q] = (PAIR || q == 0) ? mat_n(q, s + 1) : n_next[0];
                 auto none = [](const Ray<double>&) {};
                 Ray<double> o[kSweepRays];
 #pragma unroll
-                for (int q = 0; q < kSweepRays; ++q)
-                    surface_step<double, K, A, kPosOnly>(sd, r[q], n_cur, n_next, iwl, none, o[q],
-                                                         static_cast<GuardBranch*>(nullptr), kCarry ? &rxy[q] : nullptr);
+                for (int q = 0; q < kSweepRays; ++q) {
+                    const DevSurface<double> sd = (PAIR || q == 0) ? surface_for(q, s, base) : surface_for(0, s, base);
+                    surface_step<double, K, A, kMode>(sd, r[q], n_cur[q], n_next[q], iwl[q], none, o[q],
+                                                      static_cast<GuardBranch*>(nullptr), kCarry ? &rxy[q] : nullptr);
+                }
 #pragma unroll
-                for (int q = 0; q < kSweepRays; ++q) r[q] = o[q];
-                n_cur = n_next;
+                for (int q = 0; q < kSweepRays; ++q) {
+                    r[q] = o[q];
+                    n_cur[q] = n_next[q];
+                }
                 ++s;
             } while (s < a.nsurf && code_of(s) == code);
         });
     }
-    auto reduce = [&](const Ray<double>& r, bool ok, int64_t tile) {
+    auto reduce = [&](const Ray<double>& r, bool ok, int64_t g, int64_t tile) {
         double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
         // the reference's position rule of the last surface (RT:1221 / RT:1289; a PerfectLens's after-plane
         // propagation gives a NaN position for a NaN direction by itself): NaN direction -> no spot point
@@ -238,10 +301,7 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         __syncthreads();
     };
 #pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) {
-        const int64_t tile = tile0 + q;
-        reduce(r[q], tile * kBlock + threadIdx.x < a.gsize, tile);
-    }
+    for (int q = 0; q < kSweepRays; ++q) reduce(r[q], tile[q] * kBlock + threadIdx.x < a.gsize, grp[q], tile[q]);
 }
 
 // griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
@@ -368,8 +428,32 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     const size_t ntab = size_t(n_thetas + nphis);
     const size_t S = static_cast<size_t>(plan->nsurf);
     const size_t per_group = M + 3 * S;                 // n of every material, then n_s/n_s+1, 1/n_s+1, flags
-    const size_t bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) +
-                         (pre_n ? size_t(n_groups) * per_group * sizeof(double) : 0);
+    // block rows: groups of one field point paired (the same fan at two wavelengths: one ray, two refractions at the
+    // first surface, see sweep_kernel), the rest single.  Pairs need the host-evaluated media (pre_n).
+    std::vector<int32_t> pairs, singles;
+    {
+        std::map<std::array<uint64_t, 3>, int32_t> open;       // field point (bit patterns) -> unpaired group
+        for (int64_t gi = 0; gi < n_groups; ++gi) {
+            std::array<uint64_t, 3> key;
+            std::memcpy(key.data(), group_params + 4 * gi, 3 * sizeof(double));
+            auto it = open.find(key);
+            if (pre_n && it != open.end()) {
+                pairs.push_back(it->second);
+                pairs.push_back(static_cast<int32_t>(gi));
+                open.erase(it);
+            } else if (pre_n) {
+                open[key] = static_cast<int32_t>(gi);
+            } else {
+                singles.push_back(static_cast<int32_t>(gi));
+            }
+        }
+        for (const auto& kv : open) singles.push_back(kv.second);
+        std::sort(singles.begin(), singles.end());
+    }
+    const size_t nidx = pairs.size() + singles.size();
+    const size_t gn_bytes = pre_n ? size_t(n_groups) * per_group * sizeof(double) : 0;
+    const size_t bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) + gn_bytes +
+                         nidx * sizeof(int32_t);
     void* dbuf = nullptr;
     HIP_TRY(hipMallocAsync(&dbuf, bytes, st));
     PinnedStaging& g_pinned = pinned_staging();
@@ -394,6 +478,10 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
             }
         }
     }
+    const size_t idx_off = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) + gn_bytes;
+    int32_t* hidx = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(g_pinned.buf) + idx_off);
+    std::copy(pairs.begin(), pairs.end(), hidx);
+    std::copy(singles.begin(), singles.end(), hidx + pairs.size());
     rc = g_pinned.upload(dbuf, bytes, st);
     if (rc) return rc;
     SweepArgs a{};
@@ -403,6 +491,7 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     a.tab = static_cast<const double2*>(dbuf);
     a.grp = reinterpret_cast<const double*>(static_cast<char*>(dbuf) + ntab * sizeof(double2));
     a.gn = a.grp + 4 * n_groups;
+    const int32_t* didx = reinterpret_cast<const int32_t*>(static_cast<char*>(dbuf) + idx_off);
     a.partials = workspace;
     a.n_thetas = n_thetas;
     a.nphis = nphis;
@@ -412,15 +501,25 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
     }
     a.nsurf = plan->nsurf;
-    const dim3 grid(static_cast<unsigned>((tiles + kSweepRays - 1) / kSweepRays), static_cast<unsigned>(n_groups));
     auto go = [&](auto tag) {
         using TS = decltype(tag);
-        const int f = plan->feat & 3;                 // lens / POLY6 code; tables are always compiled in here
-        if (pre_n && f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16>), grid, dim3(kBlock), 0, st, a);
-        else if (pre_n) hipLaunchKernelGGL((sweep_kernel<TS, 17>), grid, dim3(kBlock), 0, st, a);
-        else if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 0>), grid, dim3(kBlock), 0, st, a);
-        else if (f == 1) hipLaunchKernelGGL((sweep_kernel<TS, 1>), grid, dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((sweep_kernel<TS, 3>), grid, dim3(kBlock), 0, st, a);
+        const int f = plan->feat & 3;                 // lens / POLY6 code (no pre_n: POLY6); tables always compiled in
+        if (!pairs.empty()) {
+            SweepArgs ap = a;
+            ap.gidx = didx;
+            const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(pairs.size() / 2));
+            if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16, true>), grid, dim3(kBlock), 0, st, ap);
+            else hipLaunchKernelGGL((sweep_kernel<TS, 17, true>), grid, dim3(kBlock), 0, st, ap);
+        }
+        if (!singles.empty()) {
+            SweepArgs as = a;
+            as.gidx = didx + pairs.size();
+            const dim3 grid(static_cast<unsigned>((tiles + kSweepRays - 1) / kSweepRays),
+                            static_cast<unsigned>(singles.size()));
+            if (pre_n && f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16, false>), grid, dim3(kBlock), 0, st, as);
+            else if (pre_n) hipLaunchKernelGGL((sweep_kernel<TS, 17, false>), grid, dim3(kBlock), 0, st, as);
+            else hipLaunchKernelGGL((sweep_kernel<TS, 3, false>), grid, dim3(kBlock), 0, st, as);   // POLY6 media
+        }
     };
     if (plan->dtype == RTPB_F64) go(double{});
     else go(float{});

@@ -105,10 +105,9 @@ class HistoryWriter:
                 buf.copy_(history, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(stream)
-            # the copy reads `history` on the side stream: recorded for torch's allocator AND for the
-            # library's history buffers (large default histories; torch's record_stream ignores them), and
-            # the queue item holds the tensor until the copy has finished, so its memory is not handed to
-            # the next trace while the copy is in flight (the next trace takes another buffer meanwhile)
+            # the copy reads `history` on the side stream: recorded (torch's allocator; E.record_stream also
+            # covers a buffer of the library's own C-ABI pool), and the queue item holds the tensor until the
+            # copy has finished, so its memory is not handed to the next trace while the copy is in flight
             E.record_stream(history, stream)
             self._q.put((index, buf.numpy(), ev, buf, history))
         else:

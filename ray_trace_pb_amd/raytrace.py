@@ -410,27 +410,26 @@ def shard_bounds(n, n_shards):
 def history_buffer(shape, dtype, device):
     """A preallocated history for ``ray_trace(..., out=)``: a C-contiguous torch CUDA tensor of ``shape``
     ((P, N, 8), P stored planes) and ``dtype`` (torch.float32 / torch.float64) on ``device``, whose device
-    memory is mapped in shuffled 64 MiB chunks (rtpb_buffer_alloc) so that the history's many-plane writes
-    run at their fast rate wherever the memory lies."""
+    memory is mapped in shuffled 64 MiB chunks so that the history's many-plane writes run at their fast rate
+    wherever the memory lies.  It is an ordinary torch allocation (the device's history pool, a
+    torch.cuda.MemPool whose segments librtpb maps): Tensor.record_stream and torch's memory statistics apply."""
     return E.history_buffer(shape, dtype, device)
 
 
 def record_stream(tensor, stream):
-    """Mark a use of ``tensor`` on ``stream`` before it is freed -- torch's ``Tensor.record_stream``, extended
-    to history buffers (a :func:`history_buffer`, and any default history of ``POOLED_HISTORY_BYTES`` or
-    more), whose memory torch's allocator does not own: the next owner of that memory then waits for the
-    work queued on ``stream``."""
+    """Mark a use of ``tensor`` on ``stream`` before it is freed: torch's ``Tensor.record_stream`` (enough for
+    every history this package allocates), plus the library's record for a buffer of its own C-ABI pool."""
     E.record_stream(tensor, stream)
 
 
 def trim_history_buffers():
-    """Release the device memory the history-buffer pool keeps for reuse (call it with
-    ``torch.cuda.empty_cache()`` to return all cached memory to the device)."""
+    """Release the device memory the history pools cache (``torch.cuda.empty_cache()`` releases torch's default
+    pool; a history pool keeps its unused segments until this call or until another allocation needs them)."""
     E.trim_history_buffers()
 
 
 def history_buffers_held(device=-1):
-    """(bytes, buffers) of freed history buffers the pool still holds on ``device`` (-1: all devices)."""
+    """(bytes, segments) of history memory cached but not in use on ``device`` (-1: all devices)."""
     return E.history_buffers_held(device)
 
 
@@ -506,22 +505,24 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
     return E.trace_host(low, last, sel, devs)
 
 
-# histories at least this large are allocated as history buffers (placement): the many-plane
-# writes keep their fast rate whatever the physical state of the card.  Stream-ordered like torch's
-# allocator; a use on another stream is recorded with record_stream (io.HistoryWriter does it)
-POOLED_HISTORY_BYTES = 1 << 30
+# histories at least this large are allocated in the history pool (shuffled-chunk placement).  From
+# the one-process sweep of profiles/r05/b/history_threshold.log (the same trace into torch.empty and into
+# history-pool histories, 4 of each): equal up to 256 MiB, the pool 2 % faster at 512 MiB, 11 % faster at C2's
+# 671 MiB history (1M rays, float64) and 8 % faster for a quarter-size C3 history; smaller histories are single
+# chunks, where the shuffle has nothing to place.  Both are torch allocations with torch's stream rules.
+POOLED_HISTORY_BYTES = 512 << 20
 
 
 def _default_history(code, last, sel, layout_code):
-    """The result buffer of a trace without out=: a pooled history_buffer for large histories, else None
-    (trace_device then allocates with torch)."""
+    """The result buffer of a trace without out=: a history-pool tensor for large histories, else None
+    (trace_device then allocates with torch's default pool)."""
     import torch
     n = last.shape[0]
     elem = 8 if code == C.RTPB_F64 else 4
     if len(sel) * n * 8 * elem < POOLED_HISTORY_BYTES:
         return None
     shape = (len(sel), n, 8) if layout_code == C.RTPB_AOS else (len(sel), 8, n)
-    return E.history_buffer(shape, torch.float64 if elem == 8 else torch.float32, last.device)
+    return E.pool_empty(shape, torch.float64 if elem == 8 else torch.float32, last.device)
 
 
 _MISS_FLAGS = threading.local()

@@ -1,7 +1,9 @@
-"""Placement-robust history buffers (rtpb_buffer_alloc / _free / _dlpack, ABI 5; stream-ordered since ABI 6)
-and ``ray_trace(..., out=)``: the buffer is ordinary device memory to the kernels (bit-identical histories),
-a torch tensor to the caller, released when the tensor dies, and never handed to a new owner while work of
-the previous owner -- on its allocation stream or on a recorded stream -- can still touch it."""
+"""Placement-robust history buffers and ``ray_trace(..., out=)``.  Default: torch tensors of the device's history
+pool (a torch.cuda.MemPool whose segments librtpb maps in shuffled chunks, rtpb_torch_alloc / _free, ABI 7) --
+bit-identical histories, torch's own stream rules (Tensor.record_stream), statistics and out-of-memory handling.
+The C ABI's own buffers (rtpb_buffer_alloc / _free / _dlpack, ABI 5-6; ``history_buffer(..., chunk_bytes=)``)
+keep their stream-ordered pool: never handed to a new owner while work of the previous owner -- on its
+allocation stream or on a recorded stream -- can still touch them."""
 import ctypes
 import gc
 import os
@@ -69,8 +71,11 @@ def test_out_validation():
 
 
 def test_buffers_are_pooled_and_trimmed():
-    C.check(C.lib().rtpb_buffer_trim())
+    """History-pool segments are cached by torch once their tensors die (the same block comes back) and
+    released by trim_history_buffers."""
+    rt.trim_history_buffers()
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     free0 = torch.cuda.mem_get_info()[0]
     ptrs = set()
     for _ in range(4):
@@ -79,11 +84,33 @@ def test_buffers_are_pooled_and_trimmed():
         ptrs.add(t.data_ptr())
         del t
         gc.collect()
-    assert len(ptrs) == 1                                                   # the pooled buffer came back
+    assert len(ptrs) == 1                                                   # the cached block came back
     torch.cuda.synchronize()
     assert torch.cuda.mem_get_info()[0] < free0 - (28 << 30)                # ... and is still held (28.3 GiB)
-    C.check(C.lib().rtpb_buffer_trim())
+    assert rt.history_buffers_held(0)[0] >= 19 * 50_000_000 * 8 * 4
+    rt.trim_history_buffers()
     assert torch.cuda.mem_get_info()[0] >= free0 - (256 << 20)
+    assert rt.history_buffers_held(0) == (0, 0)
+
+
+def test_history_buffers_are_torch_allocations():
+    """memory_allocated counts a history-pool tensor; librtpb maps (and on release unmaps) its segment."""
+    from ray_trace_pb_amd import _engine as E
+    rt.trim_history_buffers()
+    torch.cuda.synchronize()
+    a0, s0 = torch.cuda.memory_allocated(0), E.buffer_stats(0)
+    t = rt.history_buffer((11, 1 << 24, 8), torch.float64, DEV)             # 11.8 GB
+    assert torch.cuda.memory_allocated(0) - a0 == t.numel() * 8
+    s1 = E.buffer_stats(0)
+    assert s1["segments_allocated"] == s0["segments_allocated"] + 1 and s1["pool_bytes"] >= t.numel() * 8
+    del t
+    gc.collect()
+    assert torch.cuda.memory_allocated(0) == a0
+    rt.trim_history_buffers()
+    s2 = E.buffer_stats(0)
+    assert s2["segments_freed"] == s1["segments_freed"] + 1 and s2["pool_segments"] == s0["pool_segments"]
+    # a released mapping's virtual range is never reserved again (DESIGN.md §2): counted as dead address space
+    assert s2["dead_va_bytes"] >= s1["dead_va_bytes"] + 11 * (1 << 24) * 8 * 8
 
 
 def test_buffer_abi_errors():
@@ -115,31 +142,76 @@ def test_buffer_abi_errors():
 
 
 def test_large_default_histories_are_pooled_buffers():
-    """System.ray_trace without out= allocates histories >= POOLED_HISTORY_BYTES as pooled history buffers:
-    the same buffer comes back once the previous result is dropped, and the history is bit-identical to a
-    trace into a torch.empty history."""
+    """System.ray_trace without out= allocates histories >= POOLED_HISTORY_BYTES in the history pool: the same
+    block comes back once the previous result is dropped, and the history is bit-identical to a trace into a
+    torch.empty history."""
     system, m0, m1, rays, ref = golden("c3_relay")
     fan = torch.empty((4 * 1000 * 1000, 8), dtype=torch.float64, device=DEV)
     rt.fan_into(fan, np.array([8.0, 0, 0]), np.pi / 180, 2000, 0.635, 2000)
     planes = 2 * len(system.surfaces) + 1
     assert planes * fan.shape[0] * 8 * 4 >= rt.POOLED_HISTORY_BYTES
+    from ray_trace_pb_amd import _engine as E
+    made = E.buffer_stats(0)["segments_allocated"]
     h1 = system.ray_trace(fan, m0, m1, dtype="float32")
     p1 = h1.data_ptr()
+    assert any(seg["address"] <= p1 < seg["address"] + seg["total_size"] for seg in E.history_pool(0).snapshot())
     ref_t = torch.empty_like(h1)
     system.ray_trace(fan, m0, m1, dtype="float32", out=ref_t)
-    assert torch.equal(torch.isnan(h1), torch.isnan(ref_t))
-    assert bool(((h1 == ref_t) | torch.isnan(ref_t)).all())
     assert torch.equal(h1.view(torch.int32), ref_t.view(torch.int32))
     del h1
     gc.collect()
     h2 = system.ray_trace(fan, m0, m1, dtype="float32")
     assert h2.data_ptr() == p1
+    assert E.buffer_stats(0)["segments_allocated"] <= made + 1
     assert torch.equal(h2.view(torch.int32), ref_t.view(torch.int32))
-    small = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)        # small: torch's allocator
+    small = system.ray_trace(torch.from_numpy(rays).to(DEV), m0, m1)        # small: torch's default pool
     assert same_bits(small.cpu().numpy(), ref)
     del h2
     gc.collect()
-    C.check(C.lib().rtpb_buffer_trim())
+    rt.trim_history_buffers()
+
+
+@pytest.mark.skipif(not hasattr(torch.cuda, "_sleep"), reason="torch.cuda._sleep is not available")
+def test_default_history_obeys_torch_record_stream():
+    """The lightsheet pattern with torch's own idiom (scripts/2024_04_01_lightsheet.py:51-60,134-135): a >= 1 GiB
+    default history is copied to the host on a side stream (delayed), recorded with torch's Tensor.record_stream
+    and freed while the copy is pending; the next configuration traces into a default history at once.  Both
+    read back bitwise: torch never handed the first history's memory to the second trace early."""
+    import systems
+    rt.trim_history_buffers()
+    system = systems.c3_system(rt, mat)
+    m0 = m1 = mat.Vacuum()
+    nt = nph = 1342                                          # 1,800,964 rays: 19 float32 planes = 1.02 GiB
+    P = 2 * len(system.surfaces) + 1
+    fans, refs = [], []
+    for h in (0.0, 12.0):
+        f = torch.empty((nt * nph, 8), dtype=torch.float64, device=DEV)
+        rt.fan_into(f, np.array([h, 0, 0]), np.pi / 180, nt, 0.635, nph)
+        fans.append(f)
+        r = torch.empty((P, nt * nph, 8), dtype=torch.float32, device=DEV)
+        system.ray_trace(f, m0, m1, dtype="float32", out=r)
+        refs.append(r.cpu())
+    a0 = torch.cuda.memory_allocated(0)
+    h1 = system.ray_trace(fans[0], m0, m1, dtype="float32")
+    assert h1.nbytes >= 1 << 30 and torch.cuda.memory_allocated(0) - a0 >= h1.nbytes     # torch sees it
+    host = torch.empty(h1.shape, dtype=h1.dtype, pin_memory=True)
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(400_000_000)
+        host.copy_(h1, non_blocking=True)
+    h1.record_stream(side)                                   # torch's method, nothing of this package
+    p1 = h1.data_ptr()
+    del h1
+    gc.collect()
+    h2 = system.ray_trace(fans[1], m0, m1, dtype="float32")
+    assert h2.data_ptr() != p1                               # the first history's block was still pending
+    torch.cuda.synchronize()
+    assert torch.equal(host.view(torch.int32), refs[0].view(torch.int32))
+    assert torch.equal(h2.cpu().view(torch.int32), refs[1].view(torch.int32))
+    del h2
+    gc.collect()
+    rt.trim_history_buffers()
 
 
 def _sleep_available():
@@ -161,14 +233,14 @@ def test_reuse_waits_for_the_previous_owners_allocation_stream():
     a, b = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
     shape = (3, 1 << 20, 8)
     from ray_trace_pb_amd import _engine as E
-    t = E.history_buffer(shape, torch.float32, DEV, stream=a)
+    t = E.history_buffer(shape, torch.float32, DEV, chunk_bytes=64 << 20, stream=a)
     p = t.data_ptr()
     _delay(a)
     with torch.cuda.stream(a):
         t.fill_(1.0)                       # queued behind the spin: still pending when t is freed
     del t
     gc.collect()
-    u = E.history_buffer(shape, torch.float32, DEV, stream=b)
+    u = E.history_buffer(shape, torch.float32, DEV, chunk_bytes=64 << 20, stream=b)
     assert u.data_ptr() == p               # the pooled buffer
     with torch.cuda.stream(b):
         u.fill_(2.0)                       # must run after A's fill
@@ -188,7 +260,7 @@ def test_reuse_waits_for_recorded_streams():
     a, side = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
     from ray_trace_pb_amd import _engine as E
     shape = (5, 1 << 20, 8)
-    t = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    t = E.history_buffer(shape, torch.float64, DEV, chunk_bytes=64 << 20, stream=a)
     p = t.data_ptr()
     _delay(side)
     with torch.cuda.stream(side):
@@ -196,7 +268,7 @@ def test_reuse_waits_for_recorded_streams():
     rt.record_stream(t, side)
     del t
     gc.collect()
-    u = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    u = E.history_buffer(shape, torch.float64, DEV, chunk_bytes=64 << 20, stream=a)
     assert u.data_ptr() == p
     with torch.cuda.stream(a):
         u.fill_(4.0)
@@ -216,7 +288,7 @@ def test_trace_on_a_side_stream_is_recorded():
     x = torch.from_numpy(np.tile(rays, (2000, 1))).to(DEV)
     a, side = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
     shape = (2 * len(system.surfaces) + 1, x.shape[0], 8)
-    out = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    out = E.history_buffer(shape, torch.float64, DEV, chunk_bytes=64 << 20, stream=a)
     p = out.data_ptr()
     side.wait_stream(torch.cuda.current_stream(DEV))
     with torch.cuda.stream(side):
@@ -225,7 +297,7 @@ def test_trace_on_a_side_stream_is_recorded():
         system.ray_trace(x, m0, m1, out=out)
     del out
     gc.collect()
-    u = E.history_buffer(shape, torch.float64, DEV, stream=a)
+    u = E.history_buffer(shape, torch.float64, DEV, chunk_bytes=64 << 20, stream=a)
     assert u.data_ptr() == p
     with torch.cuda.stream(a):
         u.fill_(-1.0)
@@ -237,13 +309,14 @@ def test_trace_on_a_side_stream_is_recorded():
 
 
 def test_pool_keeps_only_the_newest_buffer():
-    """After the results die, the pool holds one freed buffer per device (the newest), not every size seen:
-    memory torch cannot see stays bounded."""
-    C.check(C.lib().rtpb_buffer_trim())
+    """The C ABI's own pool (history_buffer(..., chunk_bytes=)) holds one freed buffer per device (the newest),
+    not every size seen."""
+    from ray_trace_pb_amd import _engine as E
+    rt.trim_history_buffers()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     free0 = torch.cuda.mem_get_info()[0]
-    bufs = [rt.history_buffer((k, 1 << 27, 8), torch.float32, DEV) for k in (2, 3, 4)]     # 8, 12, 16 GiB
+    bufs = [E.history_buffer((k, 1 << 27, 8), torch.float32, DEV, chunk_bytes=64 << 20) for k in (2, 3, 4)]
     for t in bufs:
         t[-1, -1].fill_(0.0)
     del bufs, t
@@ -252,41 +325,94 @@ def test_pool_keeps_only_the_newest_buffer():
     nbytes, nbuf = rt.history_buffers_held(0)
     assert nbuf == 1 and nbytes == 4 << 32                       # the last one freed: 16 GiB
     assert torch.cuda.mem_get_info()[0] >= free0 - (16 << 30) - (512 << 20)
-    C.check(C.lib().rtpb_buffer_trim())
+    rt.trim_history_buffers()
     assert torch.cuda.mem_get_info()[0] >= free0 - (512 << 20)
 
 
 def test_torch_allocation_takes_the_pooled_memory():
-    """A history allocation by torch that only fits in the memory the pool holds succeeds: on torch's
-    out-of-memory error the drop-in path releases the pool and retries (E.device_empty) -- here the
-    drop-in call itself, with a history below POOLED_HISTORY_BYTES (a torch allocation)."""
+    """A torch allocation outside the history pool that only fits in memory the pool caches succeeds: torch
+    takes the pool's cached block (MemPool use_on_oom) -- here the drop-in call itself, with a history below
+    POOLED_HISTORY_BYTES (a default-pool allocation)."""
     system, m0, m1, rays, ref = golden("c3_relay")
     from ray_trace_pb_amd import _engine as E
-    C.check(C.lib().rtpb_buffer_trim())
+    rt.trim_history_buffers()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    big = rt.history_buffer((1, 5 << 30), torch.float64, DEV)         # 40 GiB, then freed into the pool
+    big = rt.history_buffer((1, 5 << 30), torch.float64, DEV)         # 40 GiB, then cached by the pool
     big[0, -1].fill_(0.0)
     del big
     gc.collect()
     torch.cuda.synchronize()
-    assert rt.history_buffers_held(0)[1] == 1
+    assert rt.history_buffers_held(0)[0] >= 40 << 30
     fan = torch.empty((1000 * 1000, 8), dtype=torch.float64, device=DEV)
     rt.fan_into(fan, np.array([8.0, 0, 0]), np.pi / 180, 1000, 0.635, 1000)
-    want = system.ray_trace(fan, m0, m1, dtype="float32").cpu()        # 0.6 GB history
+    want = system.ray_trace(fan, m0, m1, dtype="float32").cpu()        # 0.15 GB history
     torch.cuda.synchronize()
     torch.cuda.empty_cache()                                           # its block must not be cached
     free = torch.cuda.mem_get_info()[0]
     filler = torch.empty(free - (256 << 20), dtype=torch.uint8, device=DEV)   # leave 256 MiB free
     try:
-        got = system.ray_trace(fan, m0, m1, dtype="float32")               # needs 0.6 GB: the pool's memory
-        assert rt.history_buffers_held(0) == (0, 0)
+        got = system.ray_trace(fan, m0, m1, dtype="float32")               # needs the pool's memory
         assert torch.equal(got.cpu().view(torch.int32), want.view(torch.int32))
         del got
     finally:
         del filler
         torch.cuda.empty_cache()
     assert E.device_empty((4,), torch.float32, DEV).numel() == 4
+    rt.trim_history_buffers()
+
+
+def test_dead_va_limit_falls_back_to_plain_allocations():
+    """Past rtpb_set_tuning("buffer_dead_va_limit") of never-reused virtual ranges, new history buffers are plain
+    hipMalloc allocations (the bound on reserved address space): traced into, they read back bitwise."""
+    from ray_trace_pb_amd import _engine as E
+    system, m0, m1, rays, ref = golden("c4_opm")
+    x = torch.from_numpy(rays).to(DEV)
+    lib = C.lib()
+    rt.trim_history_buffers()
+    limit0 = E.buffer_stats()["dead_va_limit"]
+    try:
+        C.check(lib.rtpb_set_tuning(b"buffer_dead_va_limit", 0))
+        plain0 = E.buffer_stats()["plain_allocs"]
+        for chunk in (0, 64 << 20):                                    # the history pool and the C ABI's pool
+            out = E.history_buffer(ref.shape, torch.float64, DEV, chunk_bytes=chunk)
+            got = system.ray_trace(x, m0, m1, out=out)
+            assert same_bits(got.cpu().numpy(), ref)
+            del out, got
+            gc.collect()
+            rt.trim_history_buffers()
+        assert E.buffer_stats()["plain_allocs"] == plain0 + 2
+    finally:
+        C.check(lib.rtpb_set_tuning(b"buffer_dead_va_limit", limit0))
+    assert E.buffer_stats()["dead_va_limit"] == limit0
+
+
+def test_release_after_unrecorded_side_stream_use_is_safe():
+    """a history released while a kernel on a stream nobody recorded still writes it must not be
+    unmapped under that kernel (releasing a mapping synchronises the device first) -- no fault, and the next
+    allocation reads back its own values."""
+    from ray_trace_pb_amd import _engine as E
+    rt.trim_history_buffers()
+    side = torch.cuda.Stream(DEV)
+    t = E.history_buffer((4, 1 << 22, 8), torch.float64, DEV, chunk_bytes=64 << 20)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        if _sleep_available():
+            torch.cuda._sleep(200_000_000)
+        t.fill_(7.0)                                          # not recorded: the library does not know
+    del t
+    gc.collect()                                              # pooled (the newest freed buffer)
+    u = E.history_buffer((5, 1 << 22, 8), torch.float64, DEV, chunk_bytes=64 << 20)
+    u.fill_(1.0)
+    del u
+    gc.collect()                                              # u pooled: t retires and is unmapped -- after a sync
+    v = E.history_buffer((6, 1 << 22, 8), torch.float64, DEV, chunk_bytes=64 << 20)
+    v.fill_(2.0)
+    torch.cuda.synchronize()
+    assert bool((v == 2.0).all())
+    del v
+    gc.collect()
+    rt.trim_history_buffers()
 
 
 def test_writer_streams_large_histories_back_to_back(tmp_path):
@@ -295,7 +421,7 @@ def test_writer_streams_large_histories_back_to_back(tmp_path):
     run on a side stream while the next configuration traces: every configuration reads back bitwise."""
     from ray_trace_pb_amd import io as rio
     import systems
-    C.check(C.lib().rtpb_buffer_trim())
+    rt.trim_history_buffers()
     system = systems.c3_system(rt, mat)
     m0 = m1 = mat.Vacuum()
     nt = nph = 1342                                         # 1,800,964 rays: 19 float32 planes = 1.02 GiB

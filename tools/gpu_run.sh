@@ -18,6 +18,10 @@
 #   pmc_c5           PMC passes of the fused C5 sweep kernel (1 field)
 #   e2e              host phases of the drop-in call (tools/e2e_phases.py)
 #   power            socket power / clock under the history kernels (tools/power_probe.py)
+#   placement        per-channel TCC write requests / stalls of the slowest and fastest of 6 C3 history buffers
+#                    (tools/placement_channels.py under rocprofv3 --pmc)
+#   placement2       the same study with per-channel / per-XCD derived counters (tools/placement_pmc.sh)
+#   counters         rocprofv3 -L (the PMC counters and their dimensions on this box)
 #   vmm              tests/native/vmm_remap_check (HIP virtual-memory remapping, no torch; built in-tree)
 #   valu             issue cost of the kernels' VALU instructions (tools/valu/valu_rates.hip, built in-tree)
 #   ab:LIB[,LIB..]   A/B of the in-tree library against experiment builds (tools/ab_variants.py, histories;
@@ -28,8 +32,10 @@ export TMPDIR=/tmp
 P=gpurun_out/${1:?usage: tools/gpu_run.sh OUT STEP...}
 shift
 mkdir -p "$P"
-step() {  # name timeout cmd...
+step() {  # name timeout cmd...  (a repeated name gets a suffix: _2, _3, ...)
   local name=$1 to=$2; shift 2
+  local base=$name k=2
+  while [ -e "$P/$name.log" ]; do name="${base}_$k"; k=$((k+1)); done
   echo "=== $name: $*" | tee -a "$P/steps.log"
   timeout -k 10 "$to" "$@" < /dev/null > "$P/$name.log" 2>&1
   local rc=$?
@@ -60,6 +66,13 @@ for s in "$@"; do
     e2e) step e2e 600 python3 tools/e2e_phases.py ;;
     valu) step valu 300 tools/valu/_build/valu_rates ;;
     vmm) step vmm 300 tests/native/_build/vmm_remap_check 10 ;;
+    counters) step counters 120 rocprofv3 -L ;;
+    placement2) step placement2 1500 bash tools/placement_pmc.sh "$P/placement2" ;;
+    placement)
+      step placement 900 rocprofv3 --pmc TCC_EA0_WRREQ TCC_EA0_WRREQ_DRAM_CREDIT_STALL TCC_EA0_WRREQ_STALL \
+        --output-format csv -d "$P/placement" -o pmc -- python3 tools/placement_channels.py --buffers 6
+      python3 tools/placement_channels.py --analyze "$P/placement" --log "$P/placement.log" > "$P/placement_analysis.txt" 2>&1
+      cat "$P/placement_analysis.txt" ;;
     power)
       for args in "--config c4:1.0 --planes all" "--config c4:1.0 --planes final" "--config c3:1.0 --planes all" \
                   "--config c3:1.0 --planes final"; do
