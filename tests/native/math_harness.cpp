@@ -87,3 +87,52 @@ extern "C" void harness_bounds(double aperture, double abs_radius, double tol, d
 
 // rcp_ok flags lower_surface (rtpb_math.h) gives a surface (kAxial = 64: the axial-geometry steps)
 extern "C" int harness_surface_flags(const rtpb_surface* s) { return lower_surface(*s).rcp_ok; }
+
+// The spot sweep's shared first surface (surface_step_pair, rtpb_math.h) against two separate steps, on the host:
+// n rays through surface s at Snell ratios ra and rb (uniform media), kPosOnly semantics.  out: [n][4][6] -- the
+// pair's two rays, then the two separate steps' rays (x, y, z, dx, dy, dz each).
+template <int K, bool AX>
+static void pair_vs_steps(const DevSurface<double>& base, double ra, double rb, const double* in, int64_t n,
+                          double* out) {
+    constexpr int kMode = kPosOnly | kUniMedia;
+    DevSurface<double> da = base, db = base;
+    da.nr = ra;
+    db.nr = rb;
+    da.rcp_ok |= 4;
+    db.rcp_ok |= 4;
+    for (int64_t i = 0; i < n; ++i) {
+        const double* a = in + 8 * i;
+        const Ray<double> r{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]};
+        const Rcp<double> iwl = make_wl_rcp(r.wl);
+        Ray<double> res[4];
+        double rxy[3] = {r.x * r.x + r.y * r.y, r.x * r.x + r.y * r.y, r.x * r.x + r.y * r.y};
+        const bool carry = K == SPHERE && AX;
+        surface_step_pair<double, K, AX, kMode>(da, r, 1.0, iwl, ra, rb, r.wl, res[0], res[1],
+                                                static_cast<GuardBranch*>(nullptr), carry ? &rxy[0] : nullptr);
+        auto none = [](const Ray<double>&) {};
+        surface_step<double, K, AX, kMode>(da, r, 1.0, 1.0, iwl, none, res[2], static_cast<GuardBranch*>(nullptr),
+                                           carry ? &rxy[1] : nullptr);
+        surface_step<double, K, AX, kMode>(db, r, 1.0, 1.0, iwl, none, res[3], static_cast<GuardBranch*>(nullptr),
+                                           carry ? &rxy[2] : nullptr);
+        for (int k = 0; k < 4; ++k) {
+            double* o = out + (i * 4 + k) * 6;
+            o[0] = res[k].x; o[1] = res[k].y; o[2] = res[k].z; o[3] = res[k].dx; o[4] = res[k].dy; o[5] = res[k].dz;
+        }
+    }
+}
+
+extern "C" int harness_pair_vs_steps(const rtpb_surface* s, double ra, double rb, const double* in, int64_t n,
+                                     double* out) {
+    const DevSurface<double> d = lower_surface(*s);
+    const bool ax = (d.rcp_ok & kAxial) != 0;
+    if (d.kind == SPHERE) {
+        if (ax) pair_vs_steps<SPHERE, true>(d, ra, rb, in, n, out);
+        else pair_vs_steps<SPHERE, false>(d, ra, rb, in, n, out);
+    } else if (d.kind == FLAT) {
+        if (ax) pair_vs_steps<FLAT, true>(d, ra, rb, in, n, out);
+        else pair_vs_steps<FLAT, false>(d, ra, rb, in, n, out);
+    } else {
+        return -1;
+    }
+    return 0;
+}

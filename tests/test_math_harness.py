@@ -104,3 +104,32 @@ def test_near_unit_sqrt_and_reciprocal_bit_formulas():
     # the window test |v - 1| <= 2^-31 keeps d inside the checked range
     inside = np.abs(v - 1.0) <= 2.0 ** -31
     assert np.abs(d[inside]).max() <= 1 << 22
+
+
+@pytest.mark.parametrize("name", ["c5_odt", "c3_relay", "stress", "fuzz_03", "fuzz_23"])
+def test_sweep_pair_step_equals_two_steps(name):
+    """The spot sweep's shared first surface (surface_step_pair: one intersection, normal, tests and tangent basis,
+    two refractions) gives each wavelength's ray bit for bit what its own surface_step gives (positions and
+    directions, NaN pattern included), for every refracting Flat / Sphere surface of the system, on the golden
+    rays and on rays with zero, tiny, infinite and NaN components."""
+    import json
+    import systems
+    lib = harness()
+    fn = lib.harness_pair_vs_steps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    spec, rays, _ = load_case(name)
+    system, m0, m1 = system_from_json(rt, mat, json.dumps(spec))
+    rays = np.concatenate([rays, systems.stress_rays(256, seed=11)], axis=0)
+    low = E.lower(system.surfaces, [m0] + list(system.materials) + [m1], lambda: np.unique(rays[:, 7]), C.RTPB_F64)
+    tried = 0
+    for k in range(low.nsurf):
+        if low.surfaces[k].kind not in (C.RTPB_FLAT, C.RTPB_SPHERE) or not isinstance(
+                system.surfaces[k], rt.RefractingSurface):
+            continue
+        x = np.ascontiguousarray(rays, dtype=np.float64)
+        out = np.empty((x.shape[0], 4, 6))
+        assert fn(ctypes.byref(low.surfaces[k]), 1.0 / 1.5, 1.0 / 1.52, x.ctypes.data, x.shape[0], out.ctypes.data) == 0
+        assert same_bits(out[:, 0], out[:, 2]) and same_bits(out[:, 1], out[:, 3]), (name, k)
+        tried += 1
+    assert tried > 0
