@@ -122,7 +122,26 @@ struct SweepArgs {
     int64_t n_thetas, nphis, gsize, tiles;
     double c[3], ex[3], ey[3];
     int32_t nsurf;
+    // j / n_thetas as (j * nt_mul) >> nt_shift for j < 2^31 (nt_mul != 0, see sweep_divisor), else int64 division
+    uint32_t nt_mul;
+    int32_t nt_shift;
 };
+
+// Round-up multiplier for unsigned division by d of every x < 2^31 (Granlund-Montgomery): l = ceil(log2 d),
+// m = ceil(2^(31+l) / d) < 2^32, x / d = (x m) >> (31 + l) -- with e = m d - 2^(31+l) in [0, d) the product
+// overshoots x / d by x e / (d 2^(31+l)) < 2^-l <= 1 / d, less than the gap to the next integer.
+inline void sweep_divisor(int64_t d, int64_t gsize, uint32_t& mul, int32_t& shift) {
+    mul = 0;
+    shift = 0;
+    if (d <= 0 || d > 0x7fffffff || gsize > 0x7fffffff) return;
+    int l = 0;
+    while ((int64_t(1) << l) < d) ++l;
+    const uint64_t p = uint64_t(1) << (31 + l);
+    const uint64_t m = (p + uint64_t(d) - 1) / uint64_t(d);
+    if (m >> 32) return;
+    mul = static_cast<uint32_t>(m);
+    shift = 31 + l;
+}
 
 template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
@@ -159,7 +178,16 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     }
     auto gen = [&](int64_t j, const double* gp) {
         const int64_t jj = j < a.gsize ? j : 0;
-        const int64_t it = jj % a.n_thetas, ip = jj / a.n_thetas;
+        int64_t it, ip;
+        if (a.nt_mul != 0) {
+            const uint32_t x = static_cast<uint32_t>(jj);
+            const uint32_t qt = static_cast<uint32_t>((uint64_t(x) * a.nt_mul) >> a.nt_shift);
+            ip = qt;
+            it = x - qt * static_cast<uint32_t>(a.n_thetas);
+        } else {
+            it = jj % a.n_thetas;
+            ip = jj / a.n_thetas;
+        }
         const double2 t = a.tab[it], ph = a.tab[a.n_thetas + ip];
         const double ct = t.x, st = t.y, cp = ph.x, sp = ph.y;
         Ray<double> r;
@@ -194,9 +222,12 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         iwl[q] = (PAIR || q == 0) ? make_wl_rcp(r[q].wl) : iwl[0];   // every phase update's divisor, 2 pi / wl
         gn[q] = (cptr<double>)(a.gn) + grp[q] * (4 * a.nsurf + 1);
     }
+    // the group's wavelength (not r[0].wl: a row kill fills the ray's wavelength with NaN too, and the single rows'
+    // second ray takes ray 0's n)
+    const double wl0 = r[0].wl;
     auto mat_n = [&](int q, int k) -> double {
         if constexpr ((FEAT & 16) != 0) return gn[q][k];
-        else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), r[0].wl, table);
+        else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
     };
     // the surface's descriptor for ray q: with host-evaluated media, the Snell ratio and 1 / n2 of q's group (IEEE
     // division on the host)
@@ -501,6 +532,7 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         a.c[j] = center_ray[j]; a.ex[j] = ex[j]; a.ey[j] = ey[j];
     }
     a.nsurf = plan->nsurf;
+    sweep_divisor(n_thetas, gsize, a.nt_mul, a.nt_shift);
     auto go = [&](auto tag) {
         using TS = decltype(tag);
         const int f = plan->feat & 3;                 // lens / POLY6 code (no pre_n: POLY6); tables always compiled in

@@ -345,17 +345,6 @@ __device__ __forceinline__ double fastdiv_q_nofix(double a, double b, double y) 
 }
 #endif
 
-#if defined(RTPB_FASTDIV)
-// min(|a|, |b|) as one v_min_f64 with abs modifiers.  (fmin would make LLVM quiet both operands first with a
-// v_max_f64 each -- IEEE minNum on possibly signalling NaNs; the callers only compare the result, and either
-// answer for a NaN operand is safe there.)
-__device__ __forceinline__ double min_abs(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-#endif
-
 // Rcp of a divisor whose reciprocal y = RN(1/b) the host computed: quotients through it are still correctly
 // rounded (Markstein: q0 = RN(a y) is within 1 ulp of a/b, r = fma(-b, q0, a) is exact, RN(q0 + r y) =
 // RN(a/b) when y = RN(1/b)); tests/test_gpu_fastdiv.py checks it on the same adversarial operands
@@ -493,34 +482,17 @@ RTPB_HD void div3(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 // quotient for those divisors whatever the numerator.
 // SIGN = +1 / -1: the divisor is known positive / negative and the numerators finite wherever the result matters
 // (fastdiv_q_nofix: no div_fixup); 0: any divisor and numerator (div_fixup).
-// NUM: how the numerators' lower bound is tested --
-//   kNumFrexp: the smallest frexp exponent of the three >= -799 (0, inf, NaN give 0): 3 frexp + min3 + compare;
-//   kNumMin3:  min(|x|, |y|, |z|) >= 2^-800 (two v_min_f64 with abs modifiers + a compare): a zero component takes
-//              the full sequence too (exact either way) -- for vectors whose components are rarely zero (sphere
-//              normals, the tangent basis at a sphere, PerfectLens unit vectors); a NaN component is skipped by the
-//              IEEE minimum (its fast quotient is NaN, as the division's) and all-NaN fails;
-//   kNumMin2:  min(|x|, |y|) >= 2^-800, for z structurally +-0 (or NaN where x / y are not finite) -- the tangent
-//              basis of an axial surface (tangent_basis<AX>), whose zero z component the fast quotient takes exactly
-//              (fastdiv_q_nofix keeps the zero's sign).
-constexpr int kNumFrexp = 0, kNumMin3 = 1, kNumMin2 = 2;
-template <typename T, class G = GuardBranch, int SIGN = 0, int NUM = kNumFrexp>
+// (Round 5 tried min(|x|, |y|, |z|) >= 2^-800 as the numerator test -- two v_min_f64 + a compare instead of three
+// frexp + min3 + compare: fewer instructions, but C4 +7 %, C3 +3 % and the C5 sweep +1 % slower, profiles/r05/f.)
+template <typename T, class G = GuardBranch, int SIGN = 0>
 RTPB_HD void div3_norm(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
 #if defined(RTPB_FASTDIV)
     if constexpr (sizeof(T) == 8) {
-        static_assert(NUM == kNumFrexp || SIGN != 0, "the min tests are for the fixup-free quotients");
         auto q = [&](T a) { if constexpr (SIGN == 0) return fastdiv_q(a, r.b, r.y); else return fastdiv_q_nofix<SIGN>(a, r.b, r.y); };
         const T qx = q(x), qy = q(y), qz = q(z);
-        bool num_ok;
-        if constexpr (NUM == kNumFrexp) {
-            const int e = std::min(std::min(__builtin_amdgcn_frexp_exp(x), __builtin_amdgcn_frexp_exp(y)),
-                                   __builtin_amdgcn_frexp_exp(z));
-            num_ok = e >= -799;
-        } else if constexpr (NUM == kNumMin3) {
-            num_ok = min_abs(min_abs(x, y), z) >= T(0x1p-800);
-        } else {
-            num_ok = min_abs(x, y) >= T(0x1p-800);
-        }
-        const bool slow = !(r.ok & num_ok);
+        const int e = std::min(std::min(__builtin_amdgcn_frexp_exp(x), __builtin_amdgcn_frexp_exp(y)),
+                               __builtin_amdgcn_frexp_exp(z));
+        const bool slow = !(r.ok & (e >= -799));
         if constexpr (G::kDefer) {
             g->bad = g->bad || slow;
         } else {
@@ -685,15 +657,15 @@ RTPB_HD bool positive_finite(T v) {
 // Device: a norm squared in [2^-240, 2^238) takes one range test (norm2_in_range) instead of the square
 // root's, the divisor's and the class test of the NaN fix-ups -- the norm is then positive and finite, so no
 // quotient can be NaN.  The rest (0, tiny, huge, infinite and NaN norms: normal incidence, dead rows) takes
-// the full sequences and fix-ups below.  ZAX: z is structurally +-0 (the axial tangent basis, div3_norm kNumMin2).
-template <typename T, class G = GuardBranch, bool ZAX = false>
+// the full sequences and fix-ups below.
+template <typename T, class G = GuardBranch>
 RTPB_HD void unit_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 #if defined(RTPB_FASTNORM)
     if constexpr (sizeof(T) == 8 && !G::kDefer) {
         const T v = x * x + y * y + z * z;
         if (__builtin_expect(norm2_in_range(v), 1)) {
             // positive norm, finite components: the quotients need no div_fixup
-            div3_norm<T, G, 1, ZAX ? kNumMin2 : kNumMin3>(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
+            div3_norm<T, G, 1>(x, y, z, make_rcp_in_range(sqrt_core(v)), g);
         } else {
             // the compiler's correctly rounded sqrt and divisions (one straight sequence: compact code for the
             // rare lanes), then the reference's NaN -> 0
@@ -738,8 +710,8 @@ RTPB_HD int32_t bit_select(int32_t mask, int32_t a, int32_t b) {
 // steps are 2^-53; checked exhaustively for |d| <= 2^22 against NumPy in tests/test_math_harness.py), and
 // Markstein's correction with the correctly rounded reciprocal yields correctly rounded quotients -- the bits of
 // the compiler's sequences, which also round correctly.  ~11 integer operations replace two transcendental-seeded
-// sequences (rsq + 9, rcp + 4); other v take unit_or_zero.  ZAX as unit_or_zero.
-template <typename T, class G = GuardBranch, bool ZAX = false>
+// sequences (rsq + 9, rcp + 4); other v take unit_or_zero.
+template <typename T, class G = GuardBranch>
 RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 #if defined(RTPB_FASTNORM)
     if constexpr (sizeof(T) == 8 && !G::kDefer) {
@@ -752,12 +724,12 @@ RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
             const int32_t t = bit_select(neg, (3 - d) >> 2, -(d & ~1));
             const double s = __hiloint2double(0x3FF00000 + neg, d >> 1);
             const double yr = __hiloint2double(0x3FF00000 + (t >> 31), t);
-            div3_norm<T, G, 1, ZAX ? kNumMin2 : kNumMin3>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // |c| <~ 1: no fixup
+            div3_norm<T, G, 1>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // components at most ~1: no fixup
             return;
         }
     }
 #endif
-    unit_or_zero<T, G, ZAX>(x, y, z, g);
+    unit_or_zero(x, y, z, g);
 }
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
@@ -774,7 +746,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         by = ri.dz * Nx - ri.dx * Nz;
         bz = ri.dx * Ny - ri.dy * Nx;
     }
-    unit_or_zero<T, G, AX>(bx, by, bz, g);
+    unit_or_zero(bx, by, bz, g);
     if constexpr (AX) {
         cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
         cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
@@ -784,7 +756,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
         cy = Nz * bx - Nx * bz;
         cz = Nx * by - Ny * bx;
     }
-    unit_near1_or_zero<T, G, AX>(cx, cy, cz, g);
+    unit_near1_or_zero(cx, cy, cz, g);
 }
 
 // np.sign(v) * root for root >= +0 or NaN (RT:1217; 1 - m^2 is never -0): for v < 0 or v > 0 the product is
@@ -941,7 +913,7 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     if constexpr (sizeof(T) == 8 && !G::kDefer) {
         if (__builtin_expect(norm2_fast(spv), 1)) {
             const T spn = sqrt_core(spv);
-            if (spn > T(1e-12)) div3_norm<T, G, 1, kNumMin3>(spx, spy, spz, make_rcp_in_range(spn), g);   // |s| <= norm
+            if (spn > T(1e-12)) div3_norm<T, G, 1>(spx, spy, spz, make_rcp_in_range(spn), g);   // |s| <= norm
         } else {
             const T spn = sqrt(spv);                              // the compiler's full sequences
             if (spn > T(1e-12)) {
@@ -950,7 +922,7 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
         }
         if (__builtin_expect(norm2_fast(r1v), 1)) {
             r1n = sqrt_core(r1v);
-            div3_norm<T, G, 1, kNumMin3>(ux, uy, uz, make_rcp_in_range(r1n), g);   // r1n >= 2^-120 (or NaN: NaN out)
+            div3_norm<T, G, 1>(ux, uy, uz, make_rcp_in_range(r1n), g);   // r1n >= 2^-120 (or NaN: NaN out)
         } else {
             r1n = sqrt(r1v);
             if (r1n != T(0)) {
@@ -1031,16 +1003,16 @@ RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const
         if constexpr (AX) {
             // kAxial spheres have a finite shell_hi: where the on-surface test passes (the only rays whose
             // normal reaches a stored value) each |p - c| component is below sqrt(shell_hi) < 2^513, so the
-            // numerators need only the lower bound of the exact range (div3_norm kNumMin3)
+            // numerators need only the lower bound of the exact range (div3_norm's single min3 test)
             // a finite nonzero radius in the shortcut range (host bits kRPos / kRNeg): no div_fixup -- the
             // numerators of every row that survives the on-surface test are finite (above)
             const Rcp<T> iR = host_rcp(s.R, s.rR, (s.rcp_ok & 1) != 0);
             if (s.rcp_ok & kRPos) {
                 RTPB_NO_SPECULATE();
-                div3_norm<T, G, 1, kNumMin3>(Nx, Ny, Nz, iR, g);
+                div3_norm<T, G, 1>(Nx, Ny, Nz, iR, g);
             } else if (s.rcp_ok & kRNeg) {
                 RTPB_NO_SPECULATE();
-                div3_norm<T, G, -1, kNumMin3>(Nx, Ny, Nz, iR, g);
+                div3_norm<T, G, -1>(Nx, Ny, Nz, iR, g);
             } else {
                 div3_norm(Nx, Ny, Nz, iR, g);
             }
@@ -1060,7 +1032,8 @@ RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
 // AX: the surface has kAxial geometry (not for PLANE_MIRROR).
-// MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell).
+// MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell; the
+// front-side test folded into the final kill; no "at" plane: emit_at is not called).
 // rxy (kAxial spheres in kPosOnly runs): in: x x + y y of r (on_sphere's value at the previous axial surface); out:
 // the same of the intersection point, for the next one.
 constexpr int kPosOnly = 1;
@@ -1091,8 +1064,17 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             kill_if(!on_flat(ri, s), after);
         } else {
             // front-side test against input_axis uses the INCOMING ray's direction (RT:1187-1192)
-            kill_if(front_side_fails<AX, (MODE & kPosOnly) != 0>(r, s), ri);
-            emit_at(ri);
+            bool ok;
+            if constexpr ((MODE & kPosOnly) != 0) {
+                // positions only: the failure joins the on-surface kill of `after` below instead of filling ri with
+                // NaN first (6 register fills issued on every path) -- `after` is all NaN either way, and so is every
+                // later position of the row (its next intersection reads a NaN direction); emit_at is not called
+                ok = !front_side_fails<AX, true>(r, s);
+            } else {
+                kill_if(front_side_fails<AX, false>(r, s), ri);
+                emit_at(ri);
+                ok = true;
+            }
             T ratio;
             if constexpr ((MODE & kUniMedia) != 0) {
                 ratio = s.nr;
@@ -1103,9 +1085,8 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
                 ratio = n1 / n2;
             }
             after = snell<AX && KIND == FLAT, kTirFill>(ri, Nx, Ny, Nz, ratio, g);
-            bool ok;
-            if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy);
-            else ok = on_flat<AX>(ri, s);
+            if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy) && ok;    // (rxy is written either way)
+            else ok = on_flat<AX>(ri, s) && ok;
             kill_if(!ok, after);
         }
     }
@@ -1123,15 +1104,15 @@ RTPB_HD void surface_step_pair(const DevSurface<T>& s, const Ray<T>& r, T n1, co
     T Nx, Ny, Nz;
     Ray<T> ri;
     hit_and_normal<T, KIND, AX>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz);
-    kill_if(front_side_fails<AX, true>(r, s), ri);
+    const bool front_ok = !front_side_fails<AX, true>(r, s);     // joins the final kill, as in surface_step
     constexpr bool kAxBasis = AX && KIND == FLAT;
     const SnellBasis<T> b = snell_basis<kAxBasis>(ri, Nx, Ny, Nz, g);
     after_a = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, ratio_a, g);
     after_b = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, ratio_b, g);
     after_b.wl = wl_b;
     bool ok;
-    if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy);
-    else ok = on_flat<AX>(ri, s);
+    if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy) && front_ok;
+    else ok = on_flat<AX>(ri, s) && front_ok;
     kill_if(!ok, after_a);
     kill_if(!ok, after_b);
 }
