@@ -64,6 +64,40 @@ struct SpotArgs {
     int64_t gsize, ngroups, tiles;
 };
 
+// Sums of R values over a block's 256 lanes in one fixed tree order -- red[t] += red[t + w] for t < w, w = 128, 64,
+// ..., 1 -- valid in thread 0.  The two levels that cross waves go through LDS (buf rows, slots 64..255; two
+// barriers), the six inside wave 0 through lane shuffles: the same additions of the same operands, without the
+// barrier, store and load of every level of an all-LDS tree.
+template <int R>
+__device__ __forceinline__ void block_tree_sum(double (&v)[R], double (*buf)[kBlock]) {
+    static_assert(kBlock == 256, "four waves");
+    const int t = threadIdx.x;
+    if (t >= 128) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) buf[j][t] = v[j];
+    }
+    __syncthreads();
+    if (t < 128) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = v[j] + buf[j][t + 128];
+        if (t >= 64) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) buf[j][t] = v[j];
+        }
+    }
+    __syncthreads();
+    if (t < 64) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) v[j] = v[j] + buf[j][t + 64];
+        // lanes >= w add values no later level reads
+#pragma unroll
+        for (int w = 32; w > 0; w >>= 1) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) v[j] = v[j] + __shfl_down(v[j], w, 64);
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void spot_partial_kernel(SpotArgs a) {
     __shared__ double red[kStats][kBlock];
@@ -77,14 +111,10 @@ __global__ __launch_bounds__(kBlock) void spot_partial_kernel(SpotArgs a) {
             v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
         }
     }
-    for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
-    __syncthreads();
-    for (int w = kBlock / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
-        __syncthreads();
+    block_tree_sum<kStats>(v, red);
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < kStats; ++k) a.partials[(g * a.tiles + tile) * kStats + k] = v[k];
     }
-    if (threadIdx.x < kStats) a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
 }
 
 __global__ __launch_bounds__(kBlock) void spot_final_kernel(SpotArgs a) {
@@ -117,7 +147,8 @@ struct SweepArgs {
     const double* __restrict__ grp;     // per group: x, y, z, wavelength
     const double* __restrict__ gn;      // FEAT bit 4: per group, n of the S+1 materials at its wavelength, then
                                         // per surface n_s / n_s+1, 1 / n_s+1 and host_rcp_ok(n_s+1) (0 / 1)
-    const int32_t* __restrict__ gidx;   // the groups of block row y: one (single) or two (PAIR) per row
+    const int32_t* __restrict__ gidx;   // single rows: the group of block row y; bundle rows: see rows
+    const int32_t* __restrict__ rows;   // bundle rows: (offset into gidx, number of groups) of block row y
     double* __restrict__ partials;
     int64_t n_thetas, nphis, gsize, tiles;
     double c[3], ex[3], ey[3];
@@ -149,33 +180,36 @@ __device__ __forceinline__ double stored(double v) { return static_cast<double>(
 // kSweepRays rays per lane, traced side by side: each surface runs one surface_step instantiation per ray in one
 // straight-line region (inside one run of equal surface codes), so independent dependency chains interleave (two:
 // -6 % vs one ray per lane); each ray's 256-ray tile is reduced separately, with the same tree as
-// spot_partial_kernel.  Single rows: block b covers tiles kSweepRays*b ... of one group.  PAIR rows (round 5): the
-// lane's two rays are the SAME ray of two groups of one field point -- the same fan at two wavelengths -- so the ray is
-// generated once, and a first refracting Flat / Sphere surface, where it is still the same ray for both, runs its
-// intersection, normal, tests and tangent basis once (surface_step_pair); only the refractions differ.
+// spot_partial_kernel.  Single rows: block b covers tiles kSweepRays*b ... of one group.
+// BUNDLE rows (round 5): 2, 4, 6 or 8 groups of one field point -- the same fan at several wavelengths.  Block b covers
+// tile b of every group of the bundle: each lane generates its ray once and, when the first surface refracts (Flat /
+// Sphere), runs the part of that surface that does not depend on the wavelength once (intersection, normal, front-side
+// and on-surface tests, tangent basis: surface_step_pair's split) into LDS; then, two groups at a time, it refracts
+// the shared state with each group's Snell ratio (snell_apply) and traces the two rays through the other surfaces.
 #ifndef RTPB_SWEEP_RPL
 #define RTPB_SWEEP_RPL 2
 #endif
 constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per block)
+constexpr int kMaxBundle = 8;                      // groups per bundle row (even)
+constexpr int kStateRows = 11;                     // bundle state per lane: x y z, N, c, c . d, N . d
 
 // Occupancy: held to >= 6 waves per SIMD (<= 80 VGPRs).  Round 3 measured 7 best (2.4 % faster than the natural
 // 83 VGPRs / 5 waves, experiments/ab_sweep_wpe*.log); with round 4's lens instantiation, fixup-free quotients and
 // x x + y y carry the sweep runs 0.379 s at 6, 0.384 s at 7, 0.401 s at 8 (profiles/r04/e/, one process,
-// bit-identical).  RTPB_SWEEP_WPE overrides it (A/B builds).
+// bit-identical); round 5's pair rows: 0.345 s at 6, 0.348 s at 5, 0.353 s at 7 (profiles/r05/g).  Bundle rows hold
+// 26 KB of LDS per block (the state, and the reduction two statistics at a time), so 6 blocks fit a CU's 160 KB.
+// RTPB_SWEEP_WPE overrides it (A/B builds).
 #ifndef RTPB_SWEEP_WPE
 #define RTPB_SWEEP_WPE 6
 #endif
 #define RTPB_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(RTPB_SWEEP_WPE, 8)))
-template <typename TS, int FEAT, bool PAIR>
+template <typename TS, int FEAT, bool BUNDLE>
 __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs a) {
-    static_assert(!PAIR || (kSweepRays == 2 && (FEAT & 16) != 0), "pairs: two rays per lane, host-evaluated media");
-    __shared__ double red[kStats][kBlock];
-    int64_t grp[kSweepRays], tile[kSweepRays];
-#pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) {
-        grp[q] = PAIR ? a.gidx[2 * blockIdx.y + q] : a.gidx[blockIdx.y];
-        tile[q] = PAIR ? int64_t(blockIdx.x) : kSweepRays * int64_t(blockIdx.x) + q;
-    }
+    static_assert(!BUNDLE || (kSweepRays == 2 && (FEAT & 16) != 0), "bundles: two rays per lane, host-evaluated media");
+    constexpr int kRedRows = BUNDLE ? 2 : kStats;
+    __shared__ double red[kRedRows][kBlock];
+    __shared__ double state[BUNDLE ? kStateRows : 1][kBlock];
+    const int tid = threadIdx.x;
     auto gen = [&](int64_t j, const double* gp) {
         const int64_t jj = j < a.gsize ? j : 0;
         int64_t it, ip;
@@ -199,32 +233,20 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         r.wl = stored<TS>(gp[3]);
         return r;
     };
-    Ray<double> r[kSweepRays];
-    if constexpr (PAIR) {
-        // the groups of a pair share the field point (the host pairs only such groups): one ray, two wavelengths
-        r[0] = gen(tile[0] * kBlock + threadIdx.x, a.grp + 4 * grp[0]);
-        r[1] = r[0];
-        r[1].wl = stored<TS>(a.grp[4 * grp[1] + 3]);
-    } else {
-#pragma unroll
-        for (int q = 0; q < kSweepRays; ++q) r[q] = gen(tile[q] * kBlock + threadIdx.x, a.grp + 4 * grp[q]);
-    }
     const cptr<DevSurface<double>> surf = (cptr<DevSurface<double>>)(a.surf);
     const cptr<DevMaterial<double>> mats = (cptr<DevMaterial<double>>)(a.mats);
     const cptr<double> table = (cptr<double>)(a.table);
+    int64_t grp[kSweepRays], tile[kSweepRays];
+    Ray<double> r[kSweepRays];
     // one wavelength per group: with FEAT bit 4 the host has evaluated every material at it (the kernel's own
-    // material_n, see rtpb_spot_sweep) and the values arrive as scalar loads
-    // single rows: every ray of the block has the group's wavelength, so the per-wavelength values of ray 0 serve all
+    // material_n, see rtpb_spot_sweep) and the values arrive as scalar loads; without it (single rows only) every ray
+    // of the block has the group's wavelength, so the per-wavelength values of ray 0 serve both
     Rcp<double> iwl[kSweepRays];
     cptr<double> gn[kSweepRays];
-#pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) {
-        iwl[q] = (PAIR || q == 0) ? make_wl_rcp(r[q].wl) : iwl[0];   // every phase update's divisor, 2 pi / wl
-        gn[q] = (cptr<double>)(a.gn) + grp[q] * (4 * a.nsurf + 1);
-    }
+    double n_cur[kSweepRays];
     // the group's wavelength (not r[0].wl: a row kill fills the ray's wavelength with NaN too, and the single rows'
     // second ray takes ray 0's n)
-    const double wl0 = r[0].wl;
+    double wl0 = 0.0;
     auto mat_n = [&](int q, int k) -> double {
         if constexpr ((FEAT & 16) != 0) return gn[q][k];
         else return material_n<double, (FEAT & 2) != 0>(load_material<double>(mats + k), wl0, table);
@@ -240,99 +262,185 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         }
         return sd;
     };
-    double n_cur[kSweepRays];
-#pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) n_cur[q] = (PAIR || q == 0) ? mat_n(q, 0) : n_cur[0];
-    // runs of consecutive surfaces of one (kind, axial) code: each run loops inside one instantiation of the
-    // surface step, so the rays' registers carry from surface to surface without the copies a per-surface
-    // join of the kind branches needs (the ODT path of C5: 12 axial spheres, a lens, a flat = 3 runs)
     auto code_of = [&](int k) { return surface_code<double>((surf + k)->kind, (surf + k)->rcp_ok); };
     constexpr int kMode = kPosOnly | ((FEAT & 16) != 0 ? kUniMedia : 0);
     // the statistics read only the final positions: the steps run with kPosOnly semantics (no TIR fill of the
-    // position -- the next surface's intersection makes it NaN, and the final plane gets the rule below), and a run
-    // of axial spheres carries x x + y y of each intersection point into the next sphere's quadratic
+    // position -- the next surface's intersection makes it NaN, and the final plane gets the rule in reduce), and a
+    // run of axial spheres carries x x + y y of each intersection point into the next sphere's quadratic.
+    // Runs of consecutive surfaces of one (kind, axial) code: each run loops inside one instantiation of the surface
+    // step, so the rays' registers carry from surface to surface without the copies a per-surface join of the kind
+    // branches needs (the ODT path of C5: 12 axial spheres, a lens, a flat = 3 runs).
     double rxy[kSweepRays];
-    int s = 0;
-    if constexpr (PAIR) {
-        // the first surface, shared by the pair when it refracts (Flat / Sphere)
-        const int code = a.nsurf > 0 ? code_of(0) : -1;
-        auto first = [&](auto kind, auto ax) {
-            constexpr int K = decltype(kind)::value;
-            constexpr bool A = decltype(ax)::value;
-            const DevSurface<double> base = load_surface<double>(surf);
-            const DevSurface<double> sd0 = surface_for(0, 0, base);
-            if constexpr (K == SPHERE && A) rxy[0] = r[0].x * r[0].x + r[0].y * r[0].y;
-            Ray<double> o0, o1;
-            surface_step_pair<double, K, A, kMode>(sd0, r[0], n_cur[0], iwl[0], sd0.nr, gn[1][a.nsurf + 1], r[1].wl, o0,
-                                                   o1, static_cast<GuardBranch*>(nullptr),
-                                                   K == SPHERE && A ? &rxy[0] : nullptr);
-            r[0] = o0;
-            r[1] = o1;
+    auto trace_from = [&](int s) {
+        while (s < a.nsurf) {
+            const int code = code_of(s);
+            dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
+                constexpr int K = decltype(kind)::value;
+                constexpr bool A = decltype(ax)::value;
+                constexpr bool kCarry = K == SPHERE && A;
+                if constexpr (kCarry) {
 #pragma unroll
-            for (int q = 0; q < kSweepRays; ++q) n_cur[q] = mat_n(q, 1);
-            s = 1;
-        };
-        using std::integral_constant;
-        if (code == 2 * SPHERE + 1) first(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
-        else if (code == 2 * SPHERE) first(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
-        else if (code == 2 * FLAT + 1) first(integral_constant<int, FLAT>(), integral_constant<bool, true>());
-        else if (code == 2 * FLAT) first(integral_constant<int, FLAT>(), integral_constant<bool, false>());
-    }
-    while (s < a.nsurf) {
-        const int code = code_of(s);
-        dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
-            constexpr int K = decltype(kind)::value;
-            constexpr bool A = decltype(ax)::value;
-            constexpr bool kCarry = K == SPHERE && A;
-            if constexpr (kCarry) {
-#pragma unroll
-                for (int q = 0; q < kSweepRays; ++q) rxy[q] = r[q].x * r[q].x + r[q].y * r[q].y;
-            }
-            do {
-                const DevSurface<double> base = load_surface<double>(surf + s);
-                double n_next[kSweepRays];
-#pragma unroll
-                for (int q = 0; q < kSweepRays; ++q) n_next[q] = (PAIR || q == 0) ? mat_n(q, s + 1) : n_next[0];
-                auto none = [](const Ray<double>&) {};
-                Ray<double> o[kSweepRays];
-#pragma unroll
-                for (int q = 0; q < kSweepRays; ++q) {
-                    const DevSurface<double> sd = (PAIR || q == 0) ? surface_for(q, s, base) : surface_for(0, s, base);
-                    surface_step<double, K, A, kMode>(sd, r[q], n_cur[q], n_next[q], iwl[q], none, o[q],
-                                                      static_cast<GuardBranch*>(nullptr), kCarry ? &rxy[q] : nullptr);
+                    for (int q = 0; q < kSweepRays; ++q) rxy[q] = r[q].x * r[q].x + r[q].y * r[q].y;
                 }
+                do {
+                    const DevSurface<double> base = load_surface<double>(surf + s);
+                    double n_next[kSweepRays];
 #pragma unroll
-                for (int q = 0; q < kSweepRays; ++q) {
-                    r[q] = o[q];
-                    n_cur[q] = n_next[q];
-                }
-                ++s;
-            } while (s < a.nsurf && code_of(s) == code);
-        });
-    }
-    auto reduce = [&](const Ray<double>& r, bool ok, int64_t g, int64_t tile) {
+                    for (int q = 0; q < kSweepRays; ++q) n_next[q] = (BUNDLE || q == 0) ? mat_n(q, s + 1) : n_next[0];
+                    auto none = [](const Ray<double>&) {};
+                    Ray<double> o[kSweepRays];
+#pragma unroll
+                    for (int q = 0; q < kSweepRays; ++q) {
+                        const DevSurface<double> sd = (BUNDLE || q == 0) ? surface_for(q, s, base)
+                                                                         : surface_for(0, s, base);
+                        surface_step<double, K, A, kMode>(sd, r[q], n_cur[q], n_next[q], iwl[q], none, o[q],
+                                                          static_cast<GuardBranch*>(nullptr),
+                                                          kCarry ? &rxy[q] : nullptr);
+                    }
+#pragma unroll
+                    for (int q = 0; q < kSweepRays; ++q) {
+                        r[q] = o[q];
+                        n_cur[q] = n_next[q];
+                    }
+                    ++s;
+                } while (s < a.nsurf && code_of(s) == code);
+            });
+        }
+    };
+    // one ray's contribution to its group's tile partial: spot_partial_kernel's tree (block_tree_sum), kRedRows
+    // statistics at a time
+    auto reduce = [&](const Ray<double>& rr, bool ok, int64_t g, int64_t t) {
         double v[kStats] = {0, 0, 0, 0, 0, 0, 0};
         // the reference's position rule of the last surface (RT:1221 / RT:1289; a PerfectLens's after-plane
         // propagation gives a NaN position for a NaN direction by itself): NaN direction -> no spot point
-        if (ok && !is_nan(r.dx)) {
-            const double x = stored<TS>(r.x), y = stored<TS>(r.y), z = stored<TS>(r.z);
+        if (ok && !is_nan(rr.dx)) {
+            const double x = stored<TS>(rr.x), y = stored<TS>(rr.y), z = stored<TS>(rr.z);
             if (x - x == 0.0 && y - y == 0.0) {
                 v[0] = 1.0; v[1] = x; v[2] = y; v[3] = z; v[4] = x * x; v[5] = y * y; v[6] = x * y;
             }
         }
-        for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] = v[k];
-        __syncthreads();
-        for (int w = kBlock / 2; w > 0; w >>= 1) {
-            if (threadIdx.x < w)
-                for (int k = 0; k < kStats; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x < kStats && tile < a.tiles)
-            a.partials[(g * a.tiles + tile) * kStats + threadIdx.x] = red[threadIdx.x][0];
-        __syncthreads();
-    };
 #pragma unroll
-    for (int q = 0; q < kSweepRays; ++q) reduce(r[q], tile[q] * kBlock + threadIdx.x < a.gsize, grp[q], tile[q]);
+        for (int k0 = 0; k0 < kStats; k0 += kRedRows) {
+            double u[kRedRows];
+#pragma unroll
+            for (int j = 0; j < kRedRows; ++j) u[j] = k0 + j < kStats ? v[k0 + j] : 0.0;
+            block_tree_sum<kRedRows>(u, red);
+            if (tid == 0 && t < a.tiles) {
+#pragma unroll
+                for (int j = 0; j < kRedRows; ++j)
+                    if (k0 + j < kStats) a.partials[(g * a.tiles + t) * kStats + k0 + j] = u[j];
+            }
+        }
+    };
+    if constexpr (!BUNDLE) {
+#pragma unroll
+        for (int q = 0; q < kSweepRays; ++q) {
+            grp[q] = a.gidx[blockIdx.y];
+            tile[q] = kSweepRays * int64_t(blockIdx.x) + q;
+            r[q] = gen(tile[q] * kBlock + tid, a.grp + 4 * grp[q]);
+        }
+        wl0 = r[0].wl;
+#pragma unroll
+        for (int q = 0; q < kSweepRays; ++q) {
+            iwl[q] = q == 0 ? make_wl_rcp(r[0].wl) : iwl[0];   // every phase update's divisor, 2 pi / wl
+            gn[q] = (cptr<double>)(a.gn) + grp[q] * (4 * a.nsurf + 1);
+        }
+#pragma unroll
+        for (int q = 0; q < kSweepRays; ++q) n_cur[q] = q == 0 ? mat_n(0, 0) : n_cur[0];
+        trace_from(0);
+#pragma unroll
+        for (int q = 0; q < kSweepRays; ++q) reduce(r[q], tile[q] * kBlock + tid < a.gsize, grp[q], tile[q]);
+    } else {
+        const int32_t off = a.rows[2 * blockIdx.y], nb = a.rows[2 * blockIdx.y + 1];
+        const int64_t t0 = blockIdx.x;
+        const Ray<double> rg = gen(t0 * kBlock + tid, a.grp + 4 * int64_t(a.gidx[off]));
+        wl0 = rg.wl;
+        const int code0 = a.nsurf > 0 ? code_of(0) : -1;
+        using std::integral_constant;
+        // fn(kind, ax) on the first surface's code when it is a refracting Flat / Sphere; false otherwise
+        auto on_first = [&](auto&& fn) {
+            if (code0 == 2 * SPHERE + 1) fn(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
+            else if (code0 == 2 * SPHERE) fn(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+            else if (code0 == 2 * FLAT + 1) fn(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+            else if (code0 == 2 * FLAT) fn(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+            else return false;
+            return true;
+        };
+        // the shared part of the first surface (surface_step_pair): a row that fails the front-side or on-surface
+        // test stores a NaN position and c . d, so each refraction of it is all NaN (as the step's kill)
+        const bool shared = on_first([&](auto kind, auto ax) {
+            constexpr int K = decltype(kind)::value;
+            constexpr bool A = decltype(ax)::value;
+            const DevSurface<double> base = load_surface<double>(surf);
+            const Rcp<double> iwl0 = make_wl_rcp(rg.wl);     // (the phase, and with it n1 and iwl0, is not kept)
+            double rxy0 = rg.x * rg.x + rg.y * rg.y;
+            double Nx, Ny, Nz;
+            Ray<double> ri;
+            hit_and_normal<double, K, A>(base, rg, 1.0, iwl0, static_cast<GuardBranch*>(nullptr),
+                                         K == SPHERE && A ? &rxy0 : nullptr, ri, Nx, Ny, Nz);
+            const bool front_ok = !front_side_fails<A, true>(rg, base);
+            constexpr bool kAxBasis = A && K == FLAT;
+            const SnellBasis<double> b = snell_basis<kAxBasis>(ri, Nx, Ny, Nz, static_cast<GuardBranch*>(nullptr));
+            bool ok;
+            if constexpr (K == SPHERE) ok = on_sphere<A>(ri, base, A ? &rxy0 : nullptr) && front_ok;
+            else ok = on_flat<A>(ri, base) && front_ok;
+            double px = ri.x, py = ri.y, pz = ri.z, cd = b.cd;
+            if (!ok) px = py = pz = cd = qnan<double>();
+            state[0][tid] = px; state[1][tid] = py; state[2][tid] = pz;
+            state[3][tid] = Nx; state[4][tid] = Ny; state[5][tid] = Nz;
+            state[6][tid] = b.cx; state[7][tid] = b.cy; state[8][tid] = b.cz;
+            state[9][tid] = cd; state[10][tid] = b.nd;
+        });
+        if (!shared) {
+            state[0][tid] = rg.x; state[1][tid] = rg.y; state[2][tid] = rg.z;
+            state[3][tid] = rg.dx; state[4][tid] = rg.dy; state[5][tid] = rg.dz;
+        }
+        for (int p = 0; p < nb; p += 2) {
+#pragma unroll
+            for (int q = 0; q < kSweepRays; ++q) {
+                grp[q] = a.gidx[off + p + q];
+                tile[q] = t0;
+                gn[q] = (cptr<double>)(a.gn) + grp[q] * (4 * a.nsurf + 1);
+                r[q].ph = 0.0;
+                r[q].wl = stored<TS>(a.grp[4 * grp[q] + 3]);
+            }
+            int s0 = 0;
+            const bool first = on_first([&](auto kind, auto ax) {
+                constexpr bool kAxBasis = decltype(ax)::value && decltype(kind)::value == FLAT;
+                Ray<double> ri;
+                ri.x = state[0][tid]; ri.y = state[1][tid]; ri.z = state[2][tid];
+                ri.dx = ri.dy = ri.dz = 0.0;
+                ri.ph = 0.0;
+                const double Nx = state[3][tid], Ny = state[4][tid], Nz = state[5][tid];
+                SnellBasis<double> b;
+                b.cx = state[6][tid]; b.cy = state[7][tid]; b.cz = state[8][tid];
+                b.cd = state[9][tid]; b.nd = state[10][tid];
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q) {
+                    ri.wl = r[q].wl;
+                    r[q] = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, gn[q][a.nsurf + 1],
+                                                        static_cast<GuardBranch*>(nullptr));
+                }
+            });
+            if (first) {
+                s0 = 1;
+            } else {
+#pragma unroll
+                for (int q = 0; q < kSweepRays; ++q) {
+                    r[q].x = state[0][tid]; r[q].y = state[1][tid]; r[q].z = state[2][tid];
+                    r[q].dx = state[3][tid]; r[q].dy = state[4][tid]; r[q].dz = state[5][tid];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kSweepRays; ++q) {
+                iwl[q] = make_wl_rcp(r[q].wl);
+                n_cur[q] = mat_n(q, s0);
+            }
+            trace_from(s0);
+#pragma unroll
+            for (int q = 0; q < kSweepRays; ++q) reduce(r[q], t0 * kBlock + tid < a.gsize, grp[q], t0);
+        }
+    }
 }
 
 // griddata(method='linear') on a regular grid + the pupil field of the PSF script (rtpb_grid_interpolate).
@@ -459,29 +567,32 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     const size_t ntab = size_t(n_thetas + nphis);
     const size_t S = static_cast<size_t>(plan->nsurf);
     const size_t per_group = M + 3 * S;                 // n of every material, then n_s/n_s+1, 1/n_s+1, flags
-    // block rows: groups of one field point paired (the same fan at two wavelengths: one ray, two refractions at the
-    // first surface, see sweep_kernel), the rest single.  Pairs need the host-evaluated media (pre_n).
-    std::vector<int32_t> pairs, singles;
+    // block rows: groups of one field point in bundles of 2..kMaxBundle (even; see sweep_kernel), the rest single.
+    // Bundles need the host-evaluated media (pre_n).
+    std::vector<int32_t> bundles, rows, singles;
     {
-        std::map<std::array<uint64_t, 3>, int32_t> open;       // field point (bit patterns) -> unpaired group
+        std::map<std::array<uint64_t, 3>, std::vector<int32_t>> by_point;   // field point (bit patterns) -> groups
         for (int64_t gi = 0; gi < n_groups; ++gi) {
             std::array<uint64_t, 3> key;
             std::memcpy(key.data(), group_params + 4 * gi, 3 * sizeof(double));
-            auto it = open.find(key);
-            if (pre_n && it != open.end()) {
-                pairs.push_back(it->second);
-                pairs.push_back(static_cast<int32_t>(gi));
-                open.erase(it);
-            } else if (pre_n) {
-                open[key] = static_cast<int32_t>(gi);
-            } else {
-                singles.push_back(static_cast<int32_t>(gi));
-            }
+            if (pre_n) by_point[key].push_back(static_cast<int32_t>(gi));
+            else singles.push_back(static_cast<int32_t>(gi));
         }
-        for (const auto& kv : open) singles.push_back(kv.second);
+        for (const auto& kv : by_point) {
+            const auto& gs = kv.second;
+            size_t k = 0;
+            while (gs.size() - k >= 2) {
+                const size_t nb = std::min<size_t>(kMaxBundle, (gs.size() - k) & ~size_t(1));
+                rows.push_back(static_cast<int32_t>(bundles.size()));
+                rows.push_back(static_cast<int32_t>(nb));
+                bundles.insert(bundles.end(), gs.begin() + k, gs.begin() + k + nb);
+                k += nb;
+            }
+            if (k < gs.size()) singles.push_back(gs[k]);
+        }
         std::sort(singles.begin(), singles.end());
     }
-    const size_t nidx = pairs.size() + singles.size();
+    const size_t nidx = bundles.size() + singles.size() + rows.size();
     const size_t gn_bytes = pre_n ? size_t(n_groups) * per_group * sizeof(double) : 0;
     const size_t bytes = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) + gn_bytes +
                          nidx * sizeof(int32_t);
@@ -511,8 +622,9 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     }
     const size_t idx_off = ntab * sizeof(double2) + size_t(4 * n_groups) * sizeof(double) + gn_bytes;
     int32_t* hidx = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(g_pinned.buf) + idx_off);
-    std::copy(pairs.begin(), pairs.end(), hidx);
-    std::copy(singles.begin(), singles.end(), hidx + pairs.size());
+    std::copy(bundles.begin(), bundles.end(), hidx);
+    std::copy(singles.begin(), singles.end(), hidx + bundles.size());
+    std::copy(rows.begin(), rows.end(), hidx + bundles.size() + singles.size());
     rc = g_pinned.upload(dbuf, bytes, st);
     if (rc) return rc;
     SweepArgs a{};
@@ -536,16 +648,17 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     auto go = [&](auto tag) {
         using TS = decltype(tag);
         const int f = plan->feat & 3;                 // lens / POLY6 code (no pre_n: POLY6); tables always compiled in
-        if (!pairs.empty()) {
+        if (!rows.empty()) {
             SweepArgs ap = a;
             ap.gidx = didx;
-            const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(pairs.size() / 2));
+            ap.rows = didx + bundles.size() + singles.size();
+            const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(rows.size() / 2));
             if (f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16, true>), grid, dim3(kBlock), 0, st, ap);
             else hipLaunchKernelGGL((sweep_kernel<TS, 17, true>), grid, dim3(kBlock), 0, st, ap);
         }
         if (!singles.empty()) {
             SweepArgs as = a;
-            as.gidx = didx + pairs.size();
+            as.gidx = didx + bundles.size();
             const dim3 grid(static_cast<unsigned>((tiles + kSweepRays - 1) / kSweepRays),
                             static_cast<unsigned>(singles.size()));
             if (pre_n && f == 0) hipLaunchKernelGGL((sweep_kernel<TS, 16, false>), grid, dim3(kBlock), 0, st, as);

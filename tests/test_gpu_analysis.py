@@ -91,7 +91,7 @@ def test_spot_sweep_matches_oracle_c5_small():
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
-@pytest.mark.parametrize("case", ["c5", "c2", "tir", "tir_last", "stress"])
+@pytest.mark.parametrize("case", ["c5", "c5_bundles", "c2", "tir", "tir_last", "stress"])
 def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     """One-kernel sweep (generate + trace + reduce) == fan kernel + trace(planes='final') + spot stats,
     bit for bit, for a lens system (C5) and a lens-free one (C2), in both storage types; several
@@ -100,9 +100,16 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     x x + y y between axial spheres: the TIR prism (total internal reflection mid-path and, in 'tir_last', at
     the final surface), and the stress system (every surface kind, a mirror, misses, aperture and NA kills,
     tabulated and polynomial materials) check those against the full-semantics trace kernel."""
+    gpb = 4
     if case == "c5":
         system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
         fields, wls, theta = systems.c5_field_points(2), [0.405, 0.532, 0.785], 0.5 * np.pi / 180
+    elif case == "c5_bundles":
+        # batches of 13 groups over 2 fields x 9 wavelengths: bundle rows of 8 and 4 groups of one field point and
+        # single rows (the odd ones out) -- the first surface's shared state serves up to 8 refractions
+        system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
+        fields, wls, theta = systems.c5_field_points(2), list(np.linspace(0.4, 0.8, 9)), 0.5 * np.pi / 180
+        gpb = 13
     elif case == "c2":
         system, m0, m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
         fields, wls, theta = [[0.0, 0.0, -5.0], [1.0, -2.0, -5.0]], list(systems.C2_WAVELENGTHS), 0.05
@@ -115,13 +122,13 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
         system, m0, m1 = systems.stress_system(rt, mat), mat.Vacuum(), mat.Vacuum()
         fields, wls, theta = [[0.0, 0.0, -10.0], [3.0, -2.0, -10.0], [-1.5, 2.5, -10.0]], [0.5, 0.6328], 0.3
     args = (system, m0, m1, fields, wls, theta, 301, 77)
-    fu, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=4, fused=True)
+    fu, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=gpb, fused=True)
     un, _ = analysis.spot_sweep(*args, device=DEV, dtype=dtype, groups_per_batch=5, fused=False)
     assert fu.keys() == un.keys()
     for k in fu:
         assert same_bits(fu[k], un[k]), k
     assert fu["count"].min() > 0
-    if case != "c5" and case != "c2":
+    if case not in ("c5", "c5_bundles", "c2"):
         assert (fu["count"] < 301 * 77).any()            # some rays of the bundle are lost on the way
 
 

@@ -6,10 +6,16 @@ OUT=$1
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 python3 tools/placement_counters.py "$OUT/counter_defs.yaml" > "$OUT/custom_counters.txt" || exit 1
-export ROCPROFILER_METRICS_PATH="$OUT/counter_defs.yaml"
-timeout -s KILL 120 rocprofv3 -L > "$OUT/list.txt" 2>&1
-echo "custom counters listed: $(grep -c 'RTPB_' "$OUT/list.txt")"
-grep -q RTPB_WR_CH00 "$OUT/list.txt" || { echo "derived counters not accepted"; exit 3; }
+# rocprofiler-sdk reads counter_defs.yaml from the directory ROCPROFILER_METRICS_PATH names (a file path is not
+# accepted: round-5 run r05_j listed none of the derived counters); the file form is tried second
+ok=0
+for path in "$OUT" "$OUT/counter_defs.yaml"; do
+  export ROCPROFILER_METRICS_PATH="$path"
+  timeout -s KILL 120 rocprofv3 -L > "$OUT/list.txt" 2>&1
+  echo "ROCPROFILER_METRICS_PATH=$path: custom counters listed: $(grep -c 'RTPB_' "$OUT/list.txt")"
+  if grep -q RTPB_WR_CH00 "$OUT/list.txt"; then ok=1; break; fi
+done
+[ $ok = 1 ] || { echo "derived counters not accepted"; exit 3; }
 run() {  # tag limit counters...
   local tag=$1 lim=$2; shift 2
   timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/probe_$tag" -o pmc -- \
