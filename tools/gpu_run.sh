@@ -19,8 +19,7 @@
 #   e2e              host phases of the drop-in call (tools/e2e_phases.py)
 #   power            socket power / clock under the history kernels (tools/power_probe.py)
 #   placement        per-channel TCC write requests / stalls of the slowest and fastest of 6 C3 history buffers
-#                    (tools/placement_channels.py under rocprofv3 --pmc)
-#   placement2       the same study with per-channel / per-XCD derived counters (tools/placement_pmc.sh)
+#                    (tools/placement_channels.py under rocprofv3 --pmc, JSON output: one value per instance)
 #   counters         rocprofv3 -L (the PMC counters and their dimensions on this box)
 #   vmm              tests/native/vmm_remap_check (HIP virtual-memory remapping, no torch; built in-tree)
 #   valu             issue cost of the kernels' VALU instructions (tools/valu/valu_rates.hip, built in-tree)
@@ -67,10 +66,9 @@ for s in "$@"; do
     valu) step valu 300 tools/valu/_build/valu_rates ;;
     vmm) step vmm 300 tests/native/_build/vmm_remap_check 10 ;;
     counters) step counters 120 rocprofv3 -L ;;
-    placement2) step placement2 1500 bash tools/placement_pmc.sh "$P/placement2" ;;
     placement)
       step placement 900 rocprofv3 --pmc TCC_EA0_WRREQ TCC_EA0_WRREQ_DRAM_CREDIT_STALL TCC_EA0_WRREQ_STALL \
-        --output-format csv -d "$P/placement" -o pmc -- python3 tools/placement_channels.py --buffers 6
+        --output-format csv json -d "$P/placement" -o pmc -- python3 tools/placement_channels.py --buffers 6
       python3 tools/placement_channels.py --analyze "$P/placement" --log "$P/placement.log" > "$P/placement_analysis.txt" 2>&1
       cat "$P/placement_analysis.txt" ;;
     power)

@@ -4,16 +4,15 @@ One process allocates several C3-size histories (30.4 GB each; the history pool'
 _engine.pool_empty), times the same trace into each (interleaved rounds, HIP events), then traces twice more into
 the slowest and twice into the fastest.  Run under `rocprofv3 --pmc` with per-instance TCC counters
 (TCC_EA0_WRREQ etc.: 16 channels x 8 XCDs) to compare the per-channel write traffic and stalls of the two
-buffers; `--analyze DIR` reads the counter_collection CSV(s) and this script's own log (its ORDER line names
-every trace dispatch in launch order).
+buffers; `--analyze DIR` reads rocprofv3's JSON output and this script's own log (its ORDER line names every trace
+dispatch in launch order).
 
-    rocprofv3 --pmc TCC_EA0_WRREQ TCC_EA0_WRREQ_DRAM_CREDIT_STALL ... -d OUT -o pmc -- \\
+    rocprofv3 --pmc TCC_EA0_WRREQ TCC_EA0_WRREQ_DRAM_CREDIT_STALL ... --output-format json -d OUT -o pmc -- \\
         python3 tools/placement_channels.py --buffers 6 > OUT/run.log
     python3 tools/placement_channels.py --analyze OUT --log OUT/run.log
 """
 import argparse
 import collections
-import csv
 import glob
 import json
 import os
@@ -76,46 +75,54 @@ def run(args):
 
 
 def analyze(args):
+    """Per-instance counters from rocprofv3's JSON output (`--output-format json`): each dispatch's records hold one
+    value per counter instance, in the order of the counter's `instances` list -- for the TCC_EA0_* counters 16
+    channels (DIMENSION_INSTANCE) x 8 XCDs (DIMENSION_XCC), the channel varying fastest.  (The CSV output sums the
+    instances; rocprofv3 -L did not accept derived per-slice counters through ROCPROFILER_METRICS_PATH, r05_j/k/l.)"""
     meta = order = None
     for line in open(args.log):
         if line.startswith("BUFFERS "):
             meta = json.loads(line[8:])
         elif line.startswith("ORDER "):
             order = json.loads(line[6:])
-    rows = collections.defaultdict(lambda: collections.defaultdict(dict))   # dispatch -> counter -> key -> value
-    for f in glob.glob(os.path.join(args.analyze, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if "trace_kernel" not in r.get("Kernel_Name", ""):
-                continue
-            key = tuple((k, r[k]) for k in sorted(r) if k.lower().startswith(("dimension", "instance", "xcc")))
-            rows[int(r["Dispatch_Id"])][r["Counter_Name"]][key] = float(r["Counter_Value"])
-    ids = sorted(rows)
-    print(f"{len(ids)} trace dispatches with counters, {len(order or [])} launches in ORDER; buffers {meta}")
-    if not ids or order is None or len(ids) != len(order):
+    paths = glob.glob(os.path.join(args.analyze, "**", "*results.json"), recursive=True)
+    if not paths or meta is None or order is None:
+        print("no JSON counter output or no BUFFERS / ORDER lines")
+        return
+    d = json.load(open(paths[0]))["rocprofiler-sdk-tool"][0]
+    names = {k["kernel_id"]: k["truncated_kernel_name"] or k["kernel_name"] for k in d["kernel_symbols"]}
+    counters = {c["id"]["handle"]: c for c in d["counters"]}
+    rows = []
+    for r in d["callback_records"]["counter_collection"]:
+        info = r["dispatch_data"]["dispatch_info"]
+        if "trace_kernel" not in names.get(info["kernel_id"], ""):
+            continue
+        per = collections.defaultdict(list)
+        for rec in r["records"]:
+            per[counters[rec["counter_id"]["handle"]]["name"]].append(rec["value"])
+        rows.append((info["dispatch_id"], {k: np.array(v) for k, v in per.items()}))
+    rows.sort(key=lambda x: x[0])
+    print(f"{len(rows)} trace dispatches with counters, {len(order)} launches in ORDER; buffers {meta}")
+    if len(rows) != len(order):
         print("cannot align dispatches with launches")
         return
+    shape = {}
+    for c in counters.values():
+        dims = {dd["name"]: dd["instance_size"] for dd in c["dimensions"]}
+        if set(dims) == {"DIMENSION_INSTANCE", "DIMENSION_XCC"}:
+            shape[c["name"]] = (dims["DIMENSION_XCC"], dims["DIMENSION_INSTANCE"])
     for label, k in (("slow", meta["slow"]), ("fast", meta["fast"])):
-        sel = [d for d, b in zip(ids, order) if b == k][-2:]
-        # derived per-slice counters (tools/placement_counters.py): one vector per family, e.g. RTPB_WR_CH00..15
-        fams = collections.defaultdict(list)
-        for c in sorted(rows[sel[0]]):
-            if c.startswith("RTPB_"):
-                fams[c.rsplit("_", 1)[0] + "_" + "".join(ch for ch in c.rsplit("_", 1)[1] if not ch.isdigit())].append(c)
-        for fam, names in sorted(fams.items()):
-            v = np.array([np.mean([sum(rows[d][c].values()) for d in sel]) for c in names])
-            m = max(v.mean(), 1e-30)
-            print(f"{label} buffer {k} ({meta['ms'][k]:.3f} ms) {fam}: sum={v.sum():.4g} cv={v.std() / m:.3f} "
-                  f"max/mean={v.max() / m:.3f} min/mean={v.min() / m:.3f} per-slice/mean={np.round(v / m, 3).tolist()}")
-        for c in sorted(rows[sel[0]]):
-            v = np.array([[rows[d][c][key] for key in sorted(rows[d][c])] for d in sel]).mean(axis=0)
-            desc = f"n={v.size} sum={v.sum():.4g}"
-            if v.size > 1:
-                desc += (f" mean={v.mean():.4g} cv={v.std() / max(v.mean(), 1e-30):.3f} max/mean="
-                         f"{v.max() / max(v.mean(), 1e-30):.3f} min/mean={v.min() / max(v.mean(), 1e-30):.3f}")
-                if v.size == 128:
-                    # 8 XCDs x 16 channels in the CSV's key order: per-channel totals over the XCDs and per-XCD totals
-                    desc += f" top5={np.round(np.sort(v)[-5:] / v.mean(), 3).tolist()}"
-            print(f"{label} buffer {k} ({meta['ms'][k]:.3f} ms) {c}: {desc}")
+        sel = [v for (_, v), b in zip(rows, order) if b == k][-2:]
+        for c in sorted(sel[0]):
+            a = np.mean([s[c] for s in sel], axis=0)
+            m = max(a.mean(), 1e-30)
+            print(f"{label} buffer {k} ({meta['ms'][k]:.3f} ms) {c}: per launch {a.sum():.4g}, over {a.size} instances "
+                  f"cv {a.std() / m:.3f} min/mean {a.min() / m:.3f} max/mean {a.max() / m:.3f}")
+            if c in shape and a.size == shape[c][0] * shape[c][1]:
+                g = a.reshape(shape[c])                     # [xcc][channel]
+                ch, xc = g.sum(0), g.sum(1)
+                print(f"    per channel / mean (16, summed over XCDs): {np.round(ch / ch.mean(), 3).tolist()}")
+                print(f"    per XCD / mean (8, summed over channels):  {np.round(xc / xc.mean(), 3).tolist()}")
 
 
 def main():
