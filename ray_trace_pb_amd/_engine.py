@@ -42,7 +42,19 @@ _memo_lock = threading.Lock()            # guards _LOWERED and _KEYS (traces may
 
 
 def _vec_key(v):
+    if type(v) is np.ndarray and v.dtype == np.float64:
+        return v.tobytes()
     return np.asarray(v, dtype=np.float64).tobytes()
+
+
+_KIND_OF_CLASS = {}                      # Surface class -> its fused-kernel kind (a class property)
+
+
+def _kind_of(s):
+    kind = _KIND_OF_CLASS.get(type(s))
+    if kind is None:
+        kind = _KIND_OF_CLASS[type(s)] = s._rtpb_kind()
+    return kind
 
 
 def _lower_key(surfaces, materials, wl, dtype):
@@ -52,7 +64,7 @@ def _lower_key(surfaces, materials, wl, dtype):
     try:
         parts = [dtype]
         for s in surfaces:
-            kind = s._rtpb_kind()
+            kind = _kind_of(s)
             p = (kind, _vec_key(s.center), _vec_key(s.input_axis), _vec_key(getattr(s, "normal", s.input_axis)),
                  float(s.aperture_rad))
             if kind == C.RTPB_SPHERE:
@@ -489,6 +501,8 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
     lib = C.lib()
     ptr, handle = ctypes.c_void_p(), ctypes.c_void_p()
     seed = next(_buffer_seed)
+    global _LIB_BUFFERS_USED
+    _LIB_BUFFERS_USED = True
     if lib.rtpb_buffer_alloc(idx, nbytes, chunk_bytes, seed, raw_stream, ctypes.byref(ptr), ctypes.byref(handle)):
         # the device may be full of blocks torch's caching allocator holds: release them and retry once
         torch.cuda.synchronize(idx)
@@ -515,6 +529,9 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
         raise
 
 
+# set once this process has made a buffer of the library's own pool (history_buffer(..., chunk_bytes=N)): only then
+# can a traced tensor lie in one, and trace_device records its launches with the library too
+_LIB_BUFFERS_USED = False
 _POOLS = {}
 _ALLOCATORS = {}            # a MemPool holds a raw pointer to its allocator: allocators live as long as the process
 _pools_lock = threading.Lock()
@@ -667,6 +684,7 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
         if cur is not None:
             out.record_stream(cur)
             rays.record_stream(cur)
-        lib.rtpb_buffer_record_stream(out.data_ptr(), stream)
-        lib.rtpb_buffer_record_stream(rays.data_ptr(), stream)
+        if _LIB_BUFFERS_USED:
+            lib.rtpb_buffer_record_stream(out.data_ptr(), stream)
+            lib.rtpb_buffer_record_stream(rays.data_ptr(), stream)
     return out

@@ -1,6 +1,6 @@
 """Host phases of the drop-in call System.ray_trace(torch rays, ...) on the device-resident bundle of a
 bench config: each phase's host time per call (lowering memo, table keys, miss flag,
-history allocation + DLPack import, launch, the miss-flag read), the call's kernel (HIP events inside the
+history allocation from the history pool (round 5: a torch MemPool) or torch.empty, launch, the miss-flag read), the call's kernel (HIP events inside the
 library), and two references -- a bare launch + synchronize into a held buffer (the floor a synchronous call
 pays), and the call without its history allocation (out=).
 
@@ -94,7 +94,7 @@ def main():
 
     # (3) the drop-in call as the bench times it, phase by phase
     for name in ("lower", "tabulated", "table_fingerprint", "previous_keys", "trace_device", "history_buffer",
-                 "distinct_wavelengths"):
+                 "distinct_wavelengths", "pool_empty", "device_empty", "history_pool", "resolve_planes"):
         wrap(E, name)
     wrap(R, "_default_history")
     item = torch.Tensor.item
