@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <type_traits>
 
 #include "rtpb.h"
@@ -607,11 +608,13 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
 // where both roots are numbers t2 <= t1, and t2 is NaN only with t1 NaN or +inf.  Hence: t2 when t2 >= 0,
 // else t1, and NaN unless the choice is in [0, inf) -- the same value, zero signs included
 // (tests/test_gpu_fastdiv.py checks it against the reference's chain on adversarial B, root).
+// One product: with u2 = -B - root, 0.5 u2 >= 0 exactly when u2 >= -2^-1074 (half the smallest denormal rounds to
+// -0, to even; NaN fails both), so the halving can follow the choice.
 template <typename T>
 RTPB_HD T sphere_root(T B, T root) {
-    const T t1 = T(0.5) * (-B + root);
-    const T t2 = T(0.5) * (-B - root);
-    T t = t2 >= T(0) ? t2 : t1;
+    const T u1 = -B + root;
+    const T u2 = -B - root;
+    T t = T(0.5) * (u2 >= -std::numeric_limits<T>::denorm_min() ? u2 : u1);
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (sizeof(T) == 8) {
         // the NaN's high word from a scalar register (a VOP2 select's first operand), not a VGPR constant
