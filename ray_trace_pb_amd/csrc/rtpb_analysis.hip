@@ -158,22 +158,6 @@ struct SweepArgs {
     int32_t nt_shift;
 };
 
-// Round-up multiplier for unsigned division by d of every x < 2^31 (Granlund-Montgomery): l = ceil(log2 d),
-// m = ceil(2^(31+l) / d) < 2^32, x / d = (x m) >> (31 + l) -- with e = m d - 2^(31+l) in [0, d) the product
-// overshoots x / d by x e / (d 2^(31+l)) < 2^-l <= 1 / d, less than the gap to the next integer.
-inline void sweep_divisor(int64_t d, int64_t gsize, uint32_t& mul, int32_t& shift) {
-    mul = 0;
-    shift = 0;
-    if (d <= 0 || d > 0x7fffffff || gsize > 0x7fffffff) return;
-    int l = 0;
-    while ((int64_t(1) << l) < d) ++l;
-    const uint64_t p = uint64_t(1) << (31 + l);
-    const uint64_t m = (p + uint64_t(d) - 1) / uint64_t(d);
-    if (m >> 32) return;
-    mul = static_cast<uint32_t>(m);
-    shift = 31 + l;
-}
-
 template <typename TS>
 __device__ __forceinline__ double stored(double v) { return static_cast<double>(static_cast<TS>(v)); }
 

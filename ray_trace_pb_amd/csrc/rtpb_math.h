@@ -510,6 +510,22 @@ RTPB_HD void div3_norm(T& x, T& y, T& z, const Rcp<T>& r, G* g = nullptr) {
     x = x / r.b; y = y / r.b; z = z / r.b;
 }
 
+// Round-up multiplier for unsigned division by d of every x < 2^31 (Granlund-Montgomery): l = ceil(log2 d),
+// m = ceil(2^(31+l) / d) < 2^32, x / d = (x m) >> (31 + l) -- with e = m d - 2^(31+l) in [0, d) the product
+// overshoots x / d by x e / (d 2^(31+l)) < 2^-l <= 1 / d, less than the gap to the next integer.
+inline void sweep_divisor(int64_t d, int64_t gsize, uint32_t& mul, int32_t& shift) {
+    mul = 0;
+    shift = 0;
+    if (d <= 0 || d > 0x7fffffff || gsize > 0x7fffffff) return;
+    int l = 0;
+    while ((int64_t(1) << l) < d) ++l;
+    const uint64_t p = uint64_t(1) << (31 + l);
+    const uint64_t m = (p + uint64_t(d) - 1) / uint64_t(d);
+    if (m >> 32) return;
+    mul = static_cast<uint32_t>(m);
+    shift = 31 + l;
+}
+
 // ------------------------------------------------------------------ Material.n (MAT:39-144)
 // WITH_POLY6 = false compiles the RTPB_POLY6 case out (its pow() calls dominate the kernel's register
 // budget); WITH_TABLE = false compiles the TABLE case out.  Either is only valid for plans without such

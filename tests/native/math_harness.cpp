@@ -136,3 +136,8 @@ extern "C" int harness_pair_vs_steps(const rtpb_surface* s, double ra, double rb
     }
     return 0;
 }
+
+// the sweep's fan-index division (rtpb_spot_sweep): multiplier and shift for divisor d and group size g
+extern "C" void harness_sweep_divisor(int64_t d, int64_t g, uint32_t* mul, int32_t* shift) {
+    sweep_divisor(d, g, *mul, *shift);
+}

@@ -133,3 +133,29 @@ def test_sweep_pair_step_equals_two_steps(name):
         assert same_bits(out[:, 0], out[:, 2]) and same_bits(out[:, 1], out[:, 3]), (name, k)
         tried += 1
     assert tried > 0
+
+
+def test_sweep_fan_index_division_is_exact():
+    """rtpb_spot_sweep divides the fan index j by n_thetas as (j * mul) >> shift (rtpb_math.h sweep_divisor):
+    exact for every j < 2^31 -- checked at the quotient boundaries (multiples of d and their neighbours), near 2^31
+    and on random indices for divisors from 1 to 2^31 - 1; no multiplier for group sizes of 2^31 or more."""
+    lib = harness()
+    fn = lib.harness_sweep_divisor
+    fn.restype = None
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32)]
+    rng = np.random.default_rng(5)
+    divisors = [1, 2, 3, 7, 64, 255, 256, 257, 3162, 3163, 10001, 46341, 65537, 1 << 20, (1 << 20) + 1,
+                (1 << 30) - 1, 1 << 30, (1 << 31) - 1] + rng.integers(1, 1 << 31, 64).tolist()
+    mul, shift = ctypes.c_uint32(), ctypes.c_int32()
+    for d in divisors:
+        fn(d, (1 << 31) - 1, ctypes.byref(mul), ctypes.byref(shift))
+        assert mul.value != 0, d
+        k = np.arange(0, min(4096, ((1 << 31) - 1) // d + 1), dtype=np.uint64)
+        j = np.concatenate([k * np.uint64(d), k * np.uint64(d) + np.uint64(d - 1), k * np.uint64(d) - np.uint64(1),
+                            np.arange((1 << 31) - 4096, 1 << 31, dtype=np.uint64),
+                            rng.integers(0, 1 << 31, 20000).astype(np.uint64)])
+        j = j[j < (1 << 31)]
+        q = (j * np.uint64(mul.value)) >> np.uint64(shift.value)
+        assert np.array_equal(q, j // np.uint64(d)), d
+    fn(3163, 1 << 31, ctypes.byref(mul), ctypes.byref(shift))
+    assert mul.value == 0                         # the kernel then divides in 64 bits
