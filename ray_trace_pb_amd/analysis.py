@@ -124,10 +124,19 @@ def _spot_sweep_fused(low, S, field_points, wavelengths, theta_max, n_thetas, np
     tiles = -(-per // 256)
     if groups_per_batch is None:
         groups_per_batch = max(1, min(G, 65535, (1 << 26) // (tiles * 7)))   # workspace <= 512 MB
+        # whole field points per batch: a field point's groups share each ray's generation and first surface
+        # (the kernel's bundle rows), so batches do not split them
+        if groups_per_batch >= nw:
+            groups_per_batch -= groups_per_batch % nw
     vec = [np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel()) for v in (c, enx, eny)]
-    # one contiguous range of groups per device; per device: workspace, statistics, its current stream
+    # one contiguous range of groups per device -- whole field points when there are enough of them (see
+    # groups_per_batch); per device: workspace, statistics, its current stream
+    if nf >= len(devs):
+        bounds = [(f0 * nw, f1 * nw) for f0, f1 in shard_bounds(nf, len(devs))]
+    else:
+        bounds = shard_bounds(G, len(devs))
     work = []
-    for (g0, g1), dev in zip(shard_bounds(G, len(devs)), devs):
+    for (g0, g1), dev in zip(bounds, devs):
         ws = torch.empty(groups_per_batch * tiles * 7, dtype=torch.float64, device=dev)
         stats = torch.empty((max(g1 - g0, 1), 7), dtype=torch.float64, device=dev)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
