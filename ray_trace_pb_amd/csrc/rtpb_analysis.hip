@@ -174,7 +174,8 @@ __device__ __forceinline__ double stored(double v) { return static_cast<double>(
 #define RTPB_SWEEP_RPL 2
 #endif
 constexpr int kSweepRays = RTPB_SWEEP_RPL;         // rays per lane (tiles per block)
-constexpr int kMaxBundle = 8;                      // groups per bundle row (even)
+// groups per bundle row: a multiple of kSweepRays (each pass of a row traces kSweepRays of its groups)
+constexpr int kMaxBundle = 8 - 8 % kSweepRays;
 constexpr int kStateRows = 11;                     // bundle state per lane: x y z, N, c, c . d, N . d
 
 // Occupancy: held to >= 6 waves per SIMD (<= 80 VGPRs).  Round 3 measured 7 best (2.4 % faster than the natural
@@ -189,7 +190,7 @@ constexpr int kStateRows = 11;                     // bundle state per lane: x y
 #define RTPB_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(RTPB_SWEEP_WPE, 8)))
 template <typename TS, int FEAT, bool BUNDLE>
 __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs a) {
-    static_assert(!BUNDLE || (kSweepRays == 2 && (FEAT & 16) != 0), "bundles: two rays per lane, host-evaluated media");
+    static_assert(!BUNDLE || (FEAT & 16) != 0, "bundles: host-evaluated media");
     constexpr int kRedRows = BUNDLE ? 2 : kStats;
     __shared__ double red[kRedRows][kBlock];
     __shared__ double state[BUNDLE ? kStateRows : 1][kBlock];
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
             state[0][tid] = rg.x; state[1][tid] = rg.y; state[2][tid] = rg.z;
             state[3][tid] = rg.dx; state[4][tid] = rg.dy; state[5][tid] = rg.dz;
         }
-        for (int p = 0; p < nb; p += 2) {
+        for (int p = 0; p < nb; p += kSweepRays) {
 #pragma unroll
             for (int q = 0; q < kSweepRays; ++q) {
                 grp[q] = a.gidx[off + p + q];
@@ -551,7 +552,8 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
     const size_t ntab = size_t(n_thetas + nphis);
     const size_t S = static_cast<size_t>(plan->nsurf);
     const size_t per_group = M + 3 * S;                 // n of every material, then n_s/n_s+1, 1/n_s+1, flags
-    // block rows: groups of one field point in bundles of 2..kMaxBundle (even; see sweep_kernel), the rest single.
+    // block rows: groups of one field point in bundles of kSweepRays..kMaxBundle (multiples of kSweepRays; see
+    // sweep_kernel), the rest single.
     // Bundles need the host-evaluated media (pre_n).
     std::vector<int32_t> bundles, rows, singles;
     {
@@ -565,14 +567,15 @@ int rtpb_spot_sweep(const rtpb_plan* plan_c, int32_t device, int64_t n_groups, c
         for (const auto& kv : by_point) {
             const auto& gs = kv.second;
             size_t k = 0;
-            while (gs.size() - k >= 2) {
-                const size_t nb = std::min<size_t>(kMaxBundle, (gs.size() - k) & ~size_t(1));
+            while (gs.size() - k >= size_t(kSweepRays)) {
+                const size_t left = gs.size() - k;
+                const size_t nb = std::min<size_t>(kMaxBundle, left - left % kSweepRays);
                 rows.push_back(static_cast<int32_t>(bundles.size()));
                 rows.push_back(static_cast<int32_t>(nb));
                 bundles.insert(bundles.end(), gs.begin() + k, gs.begin() + k + nb);
                 k += nb;
             }
-            if (k < gs.size()) singles.push_back(gs[k]);
+            for (; k < gs.size(); ++k) singles.push_back(gs[k]);
         }
         std::sort(singles.begin(), singles.end());
     }
