@@ -667,7 +667,10 @@ def run_c5(args, dev, rank, world):
                       flops_per_ray=fl["flops_per_ray"], f64_wave_instructions_sample=fl["f64_wave_instructions"],
                       pmc_sample_rays=fl["pmc_sample_rays"],
                       flops_method="PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes (FMA = 2) on a 1-field "
-                                   "sweep, scaled per ray",
+                                   "sweep, scaled per ray: the float64 work the kernel executes, which the bundle rows "
+                                   "cut by sharing each ray's generation and first surface between a field point's "
+                                   "wavelengths -- so frac falls as the sweep gets faster; frac_issue is the measure "
+                                   "of how close the kernel runs to its instruction-issue ceiling",
                       valu_per_ray_surface=per_rs(mix["SQ_INSTS_VALU"]),
                       valu_mix_per_ray_surface={
                           "f64_add_mul_fma": per_rs(sum(fl["f64_wave_instructions"][k] for k in F64_COUNTERS[:3])),
