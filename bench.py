@@ -75,8 +75,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5"],
-                    help="headline workload (c5: --pmc-child only)")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c4", "c5", "c5_1wl"],
+                    help="headline workload (c5, c5_1wl: --pmc-child only)")
     ap.add_argument("--configs", default="c2,c4,c5", help="other BASELINE configs in the same line ('none')")
     ap.add_argument("--scale", type=float, default=1.0, help="c3 / c4: fraction of the per-axis fan sizes")
     ap.add_argument("--rays", type=int, default=1_000_000, help="c2: rays per GPU")
@@ -470,14 +470,25 @@ def measure_c5_flops(args):
     if err:
         return None, err
     tot = {k: sum(v) for k, v in vals.items()}
-    flops = 64.0 * (2 * tot["SQ_INSTS_VALU_FMA_F64"] + tot["SQ_INSTS_VALU_MUL_F64"] + tot["SQ_INSTS_VALU_ADD_F64"] +
-                    tot["SQ_INSTS_VALU_TRANS_F64"])
+
+    def f64_flops(t):
+        return 64.0 * (2 * t["SQ_INSTS_VALU_FMA_F64"] + t["SQ_INSTS_VALU_MUL_F64"] + t["SQ_INSTS_VALU_ADD_F64"] +
+                       t["SQ_INSTS_VALU_TRANS_F64"])
     rays = 7 * C5_FAN[0] * C5_FAN[1]
     trans = tot["SQ_INSTS_VALU_TRANS_F64"]
     cycles = (tot["SQ_INSTS_VALU"] - trans) * ISSUE_CYCLES["valu"] + trans * ISSUE_CYCLES["trans_f64"]
-    return {"flops_per_ray": flops / rays, "f64_wave_instructions": {k: tot[k] for k in F64_COUNTERS},
-            "valu_mix_wave_instructions": {k: tot[k] for k in MIX_COUNTERS}, "pmc_sample_rays": rays,
-            "issue_simd_cycles_per_ray": cycles / rays}, None
+    res = {"executed_flops_per_ray": f64_flops(tot) / rays, "f64_wave_instructions": {k: tot[k] for k in F64_COUNTERS},
+           "valu_mix_wave_instructions": {k: tot[k] for k in MIX_COUNTERS}, "pmc_sample_rays": rays,
+           "issue_simd_cycles_per_ray": cycles / rays}
+    # the algorithmic FLOPs of a ray: the same sweep at one wavelength, where every ray is traced alone (the bundle
+    # rows share generation and the first surface between a field point's wavelengths, which removes executed work)
+    one, err1 = _pmc_run(args, "c5_1wl", list(F64_COUNTERS), "sweep_kernel")
+    if err1:
+        res["flops_per_ray"], res["flops_kind"] = res["executed_flops_per_ray"], f"executed ({err1})"
+    else:
+        res["flops_per_ray"] = f64_flops({k: sum(v) for k, v in one.items()}) / (C5_FAN[0] * C5_FAN[1])
+        res["flops_kind"] = "algorithmic"
+    return res, None
 
 
 def roofline(wl, kernel_ms, traffic=None, traffic_note=None, fill=None, copy=None):
@@ -664,13 +675,18 @@ def run_c5(args, dev, rank, world):
             per_rs = lambda v: v * 64.0 / (fl["pmc_sample_rays"] * S14)       # wave-instructions -> per ray-surface
             issue_s = fl["issue_simd_cycles_per_ray"] * rays0 / SIMDS / PEAK_CLOCK_HZ
             rl.update(achieved=fl["flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
-                      flops_per_ray=fl["flops_per_ray"], f64_wave_instructions_sample=fl["f64_wave_instructions"],
+                      flops_per_ray=fl["flops_per_ray"], flops_kind=fl["flops_kind"],
+                      executed_flops_per_ray=fl["executed_flops_per_ray"],
+                      achieved_executed=fl["executed_flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
+                      f64_wave_instructions_sample=fl["f64_wave_instructions"],
                       pmc_sample_rays=fl["pmc_sample_rays"],
-                      flops_method="PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes (FMA = 2) on a 1-field "
-                                   "sweep, scaled per ray: the float64 work the kernel executes, which the bundle rows "
-                                   "cut by sharing each ray's generation and first surface between a field point's "
-                                   "wavelengths -- so frac falls as the sweep gets faster; frac_issue is the measure "
-                                   "of how close the kernel runs to its instruction-issue ceiling",
+                      flops_method="algorithmic FLOPs per ray: PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes "
+                                   "(FMA = 2) of a 1-field sweep at ONE wavelength, where every ray is traced alone, "
+                                   "scaled per ray (the analogue of algorithmic vs physical bytes); "
+                                   "executed_flops_per_ray: the same counters on the 1-field x 7-wavelength sample, "
+                                   "where the bundle rows share each ray's generation and first surface between a "
+                                   "field point's wavelengths; frac_issue: how close the kernel runs to its "
+                                   "instruction-issue ceiling",
                       valu_per_ray_surface=per_rs(mix["SQ_INSTS_VALU"]),
                       valu_mix_per_ray_surface={
                           "f64_add_mul_fma": per_rs(sum(fl["f64_wave_instructions"][k] for k in F64_COUNTERS[:3])),
@@ -692,14 +708,15 @@ def run_c5(args, dev, rank, world):
 def pmc_child(args, dev):
     """Target of the rocprofv3 --pmc child runs: a few launches of one config's kernel."""
     import torch
-    if args.config == "c5":
+    if args.config in ("c5", "c5_1wl"):
         import ray_trace_pb_amd.materials as mat
         import ray_trace_pb_amd.raytrace as rt
         from ray_trace_pb_amd import analysis
         import systems
+        # c5_1wl: one wavelength, so every ray is traced alone (no bundle sharing) -- the algorithmic FLOPs per ray
+        wls = systems.C5_WAVELENGTHS if args.config == "c5" else systems.C5_WAVELENGTHS[3:4]
         analysis.spot_sweep(systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1),
-                            systems.c5_field_points(8)[:1], systems.C5_WAVELENGTHS, 0.5 * np.pi / 180, C5_FAN[0],
-                            C5_FAN[1], device=dev)
+                            systems.c5_field_points(8)[:1], wls, 0.5 * np.pi / 180, C5_FAN[0], C5_FAN[1], device=dev)
     else:
         wl = Workload(args.config, dev, 0, scale=args.scale, c2_rays=args.rays)
         for _ in range(3):
