@@ -306,7 +306,9 @@ int rtpb_spot_stats(int32_t device, int32_t dtype, const void* plane, int64_t gr
    ex/ey and the (cos, sin) tables as for rtpb_ray_fan_tables (host).  workspace: device doubles,
    >= n_groups * ceil(n_thetas*nphis / 256) * 7.  stats_out: device, n_groups x 7.  The statistics are
    bit-identical to rtpb_ray_fan_tables + rtpb_trace (final plane) + rtpb_spot_stats in the plan's
-   storage type. */
+   storage type.  Groups with the same field point (bit for bit) are swept together -- each ray generated once
+   and, when the first surface is a refracting flat or sphere, its wavelength-independent part computed once --
+   so a call should hold all the wavelengths of its field points (order does not matter). */
 int rtpb_spot_sweep(const rtpb_plan* plan, int32_t device, int64_t n_groups, const double* group_params,
                     int64_t n_thetas, int64_t nphis, const double center_ray[3], const double ex[3],
                     const double ey[3], const double* theta_cos_sin, const double* phi_cos_sin, double* workspace,
