@@ -247,6 +247,22 @@ def test_spot_sweep_over_devices_is_bitwise_equal():
         assert all(p["kernel_ms"] > 0 for p in tm["per_device"])
 
 
+def test_spot_sweep_group_order_does_not_matter():
+    """rtpb_spot_sweep gathers the groups of one field point into bundle rows whatever their order: fields and
+    wavelengths given in another order (groups interleaved differently in one batch) give the same statistics,
+    bit for bit, in the new order."""
+    system = systems.c5_system(rt, mat)
+    fields = systems.c5_field_points(2)
+    wls = [0.405, 0.465, 0.532, 0.561, 0.785]
+    theta, nt, nph = 0.5 * np.pi / 180, 61, 29
+    ref, _ = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields, wls, theta, nt, nph, device=DEV)
+    fo, wo = [2, 0, 3, 1], [3, 1, 4, 0, 2]
+    got, _ = analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields[fo], [wls[k] for k in wo], theta,
+                                 nt, nph, device=DEV, groups_per_batch=7)      # batches of 7 mix field points
+    for k in ("count", "centroid", "rms_radius"):
+        assert same_bits(got[k], ref[k][fo][:, wo]), k
+
+
 def fixed_order_sums(plane, group_size, tile=256):
     """The spot kernels' reduction restated in NumPy, operation for operation (csrc/rtpb_analysis.hip
     spot_partial_kernel / sweep_kernel + spot_final_kernel): per 256-ray tile a pairwise tree
