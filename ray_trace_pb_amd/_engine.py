@@ -98,15 +98,15 @@ def _pure_n(m):
     return type(m).n.__module__ == __package__ + ".materials" or getattr(type(m), "rtpb_pure_n", False) is True
 
 
-def lower(surfaces, materials, wavelengths, dtype):
+def lower(surfaces, materials, wavelengths, dtype, tab=None):
     """Lower surfaces (len S) and materials (len S+1: initial, System.materials, final).
     ``wavelengths`` is a callable returning the distinct wavelengths of the bundle (used only for
     user Material subclasses, which lower to per-wavelength tables).  Results are memoised by content
-    (_lower_key); the Lowered object is read-only once built."""
+    (_lower_key); the Lowered object is read-only once built.  ``tab``: tabulated(materials) when the caller has it."""
     if len(materials) != len(surfaces) + 1:
         raise ValueError("length of materials should be len(surfaces) + 1")
     wl = None
-    if tabulated(materials):
+    if tabulated(materials) if tab is None else tab:
         wl = np.asarray(wavelengths(), dtype=np.float64)
     key = _lower_key(surfaces, materials, wl, dtype)
     if key is not None:
@@ -428,8 +428,14 @@ def input_code(dt):
     """Element type the kernel reads the input rays in: float32 rays as they are (widened exactly in
     the kernel, as NumPy promotes them in the reference), everything else as float64.  Independent of
     the storage type, so float64 rays are never rounded before the arithmetic."""
-    name = str(dt).replace("torch.", "")
-    return C.RTPB_F32 if name == "float32" else C.RTPB_F64
+    code = _INPUT_CODES.get(dt)
+    if code is None:
+        name = str(dt).replace("torch.", "")
+        code = _INPUT_CODES[dt] = C.RTPB_F32 if name == "float32" else C.RTPB_F64
+    return code
+
+
+_INPUT_CODES = {}
 
 
 def trace_host(low, rays2d, planes, devices=None, out=None):
@@ -567,10 +573,11 @@ def pool_empty(shape, dtype, device, stream=None):
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     pool = history_pool(idx)
-    with torch.cuda.device(idx):
+    dev_ctx = torch.cuda.device(idx) if idx != torch.cuda.current_device() else contextlib.nullcontext()
+    with dev_ctx:
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx, torch.cuda.use_mem_pool(pool, idx):
-            return torch.empty(shape, dtype=dtype, device=torch.device("cuda", idx))
+            return torch.empty(shape, dtype=dtype, device=dev if dev.index is not None else torch.device("cuda", idx))
 
 
 def buffer_stats(device=-1):
@@ -659,7 +666,9 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     import torch
     tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
     in_code = input_code(rays.dtype)
-    rays = rays.to(dtype=torch.float32 if in_code == C.RTPB_F32 else torch.float64).contiguous()
+    want = torch.float32 if in_code == C.RTPB_F32 else torch.float64
+    if rays.dtype != want or not rays.is_contiguous():
+        rays = rays.to(dtype=want).contiguous()
     n = rays.shape[0]
     if out is None:
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)

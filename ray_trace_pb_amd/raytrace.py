@@ -564,7 +564,7 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layou
 
     tab = E.tabulated(materials)
     if not tab:
-        return run(E.lower(surfaces, materials, None, code))
+        return run(E.lower(surfaces, materials, None, code, tab=tab))
     fp = E.table_fingerprint(tab)
     prev = E.previous_keys(fp)
     if prev is not None:
