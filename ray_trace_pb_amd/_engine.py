@@ -75,7 +75,9 @@ def _lower_key(surfaces, materials, wl, dtype):
         for m in materials:
             lowered = m._rtpb_lower() if hasattr(m, "_rtpb_lower") else None
             if lowered is not None:
-                parts.append((lowered[0], tuple(float(c) for c in lowered[1])))
+                # (an immutable tuple of numbers is its own key)
+                c = lowered[1]
+                parts.append((lowered[0], c if type(c) is tuple else tuple(map(float, c))))
             else:
                 # a tabulated material's n() values are memoised only when n() is known to depend on the
                 # wavelength and the instance's attributes alone: the package's own (Ebaf11), or a user

@@ -258,3 +258,32 @@ def test_wavelength_column_follows_numpy_assignment():
     assert rt._wavelength_column(0.5, 10) is None and rt._wavelength_column(np.array([0.5]), 10) is None
     with pytest.raises(ValueError):
         rt._wavelength_column(np.ones(4), 3)
+
+
+def test_lowering_memo_follows_in_place_changes():
+    """The lowering memo is keyed by content: a system changed in place between traces (a material's index, a
+    surface's radius, a center array edited element-wise) is lowered again, and changing it back finds the first
+    lowering."""
+    system = systems.c2_system(rt, mat)
+    mats = [mat.Vacuum()] + list(system.materials) + [mat.Vacuum()]
+    low0 = E.lower(system.surfaces, mats, None, C.RTPB_F64)
+    assert E.lower(system.surfaces, mats, None, C.RTPB_F64) is low0
+    const = mat.Constant(1.5)
+    mats2 = mats[:1] + [const] + mats[2:]
+    a = E.lower(system.surfaces, mats2, None, C.RTPB_F64)
+    const._n = 1.6
+    b = E.lower(system.surfaces, mats2, None, C.RTPB_F64)
+    assert b is not a and bytes(b.materials) != bytes(a.materials)
+    sph = next(s for s in system.surfaces if isinstance(s, rt.SphericalSurface))
+    r0 = sph.radius
+    sph.radius = r0 * 1.01
+    c = E.lower(system.surfaces, mats, None, C.RTPB_F64)
+    assert c is not low0 and bytes(c.surfaces) != bytes(low0.surfaces)
+    sph.radius = r0
+    assert E.lower(system.surfaces, mats, None, C.RTPB_F64) is low0
+    z0 = system.surfaces[-1].center[2]
+    system.surfaces[-1].center[2] = z0 + 1.0
+    d = E.lower(system.surfaces, mats, None, C.RTPB_F64)
+    assert d is not low0 and bytes(d.surfaces) != bytes(low0.surfaces)
+    system.surfaces[-1].center[2] = z0
+    assert E.lower(system.surfaces, mats, None, C.RTPB_F64) is low0
