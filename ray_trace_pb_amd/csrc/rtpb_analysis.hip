@@ -165,11 +165,13 @@ __device__ __forceinline__ double stored(double v) { return static_cast<double>(
 // straight-line region (inside one run of equal surface codes), so independent dependency chains interleave (two:
 // -6 % vs one ray per lane); each ray's 256-ray tile is reduced separately, with the same tree as
 // spot_partial_kernel.  Single rows: block b covers tiles kSweepRays*b ... of one group.
-// BUNDLE rows (round 5): 2, 4, 6 or 8 groups of one field point -- the same fan at several wavelengths.  Block b covers
-// tile b of every group of the bundle: each lane generates its ray once and, when the first surface refracts (Flat /
-// Sphere), runs the part of that surface that does not depend on the wavelength once (intersection, normal, front-side
-// and on-surface tests, tangent basis: surface_step_pair's split) into LDS; then, two groups at a time, it refracts
-// the shared state with each group's Snell ratio (snell_apply) and traces the two rays through the other surfaces.
+// BUNDLE rows (round 5): up to kMaxBundle groups of one field point (a multiple of kSweepRays: 2, 4, 6 or 8) -- the same
+// fan at several wavelengths.  Block b covers tile b of every group of the bundle: each lane generates its ray once
+// and, when the first surface refracts (Flat / Sphere), runs the part of that surface that does not depend on the
+// wavelength once (intersection, normal, front-side and on-surface tests, tangent basis: surface_step_pair's split)
+// into LDS; then, kSweepRays groups at a time, it refracts the shared state with each group's Snell ratio
+// (snell_apply) and traces those rays side by side through the other surfaces.  A field point's leftover groups run
+// in single rows.
 #ifndef RTPB_SWEEP_RPL
 #define RTPB_SWEEP_RPL 2
 #endif
