@@ -533,6 +533,15 @@ def _gather(world, vals):
     return [o.tolist() for o in out]
 
 
+def strong_scaling(t1_ms, tn_ms, world):
+    """Strong-scaling fields of a config traced whole on one GPU (t1_ms per step, rank 0 alone, before the sharded
+    run in the same job) and sharded over `world` ranks (tn_ms per step, max over ranks):
+    efficiency = t1 / (N tN) -- 1.0 is linear scaling."""
+    return {"t1_ms": t1_ms, "tN_ms": tn_ms, "speedup": t1_ms / tn_ms, "scaling_efficiency": t1_ms / (world * tn_ms),
+            "scaling_method": "t1: the whole config on rank 0's GPU alone, timed in this job before the sharded run "
+                              "(same box); tN: the sharded run's max-over-ranks step time; efficiency = t1 / (N tN)"}
+
+
 def host_e2e(w, reps=3):
     """the end-to-end rate with the PCIe transfers -- System.ray_trace on a NumPy bundle in host
     memory returning the NumPy history (rtpb_trace_host: pinned staging, chunked H2D / trace / D2H)."""
@@ -581,12 +590,28 @@ def run_c2(args, dev, copy):
 
 
 def run_c4(args, dev, rank, world, copy):
-    """BASELINE configs[3]: the 100M-ray OPM fan strong-scaled over the ranks (each rank its phi rows)."""
+    """BASELINE configs[3]: the 100M-ray OPM fan strong-scaled over the ranks (each rank its phi rows).  With N > 1
+    rank 0 first traces the whole fan alone (N = 1 in the same job, so the line carries its own scaling
+    efficiency), the other ranks waiting at a barrier."""
     import torch
+    steps = max(3, min(args.steps, 20))
+    t1_ms = None
+    if world > 1:
+        if rank == 0:
+            _log("c4: the whole fan on rank 0 alone (t1)")
+            w1 = Workload("c4", dev, 0, world=1, scale=args.scale)
+            for _ in range(max(2, min(args.warmup, 5))):
+                w1.step()
+            torch.cuda.synchronize()
+            _, wall1 = w1.timed(steps)
+            t1_ms = wall1 / steps * 1e3
+            del w1
+            torch.cuda.empty_cache()
+            _trim_buffers()
+        _barrier(world)
     wl = Workload("c4", dev, rank, world=world, scale=args.scale)
     for _ in range(max(2, min(args.warmup, 5))):
         wl.step()
-    steps = max(3, min(args.steps, 20))
     _barrier(world)
     kernel_ms, wall = wl.timed(steps)
     _barrier(world)
@@ -611,6 +636,8 @@ def run_c4(args, dev, rank, world, copy):
                "per_rank": per_rank}
         if world == 1:
             res["roofline"]["note"] = "N=1: the whole 100M-ray fan on one GPU (80 GB in HBM)"
+        else:
+            res.update(strong_scaling(t1_ms, res["ms_per_step"], world))
     del wl
     torch.cuda.empty_cache()
     _trim_buffers()
@@ -632,6 +659,20 @@ def run_c5(args, dev, rank, world):
     wls = systems.C5_WAVELENGTHS
     theta = 0.5 * np.pi / 180
     analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), mine[:1], wls, theta, 33, 32, device=dev)
+    t1_ms = None
+    if world > 1:
+        # the whole sweep on rank 0 alone first (N = 1 in the same job: the line's own scaling efficiency)
+        if rank == 0:
+            _log("c5: every field point on rank 0 alone (t1)")
+            w1 = []
+            for _ in range(args.c5_steps):
+                t0 = time.perf_counter()
+                analysis.spot_sweep(system, mat.Constant(1), mat.Constant(1), fields, wls, theta, C5_FAN[0],
+                                    C5_FAN[1], device=dev)
+                torch.cuda.synchronize()
+                w1.append(time.perf_counter() - t0)
+            t1_ms = float(np.median(w1)) * 1e3
+        _barrier(world)
     kms, walls, hbm = [], [], 0.0
     summ = None
     for _ in range(args.c5_steps):
@@ -663,6 +704,8 @@ def run_c5(args, dev, rank, world):
         "total_rays": int(total), "surfaces": S, "parallelism": f"field-point shards x{world} (no collective)",
         "per_rank": per_rank,
         "rms_radius_um_field0": (summ["rms_radius"][0] * 1e3).tolist() if rank == 0 else None}
+    if world > 1:
+        res.update(strong_scaling(t1_ms, res["ms_per_step"], world))
     rl = {"bound": "valu_f64", "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "sweep_kernel",
           "kernel_ms_max_rank": kmax, "hbm_GBps_max_rank": max(p["hbm_GBps"] for p in per_rank),
           "hbm_note": "the rays never leave registers: HBM carries only the per-tile partial sums"}
@@ -674,18 +717,19 @@ def run_c5(args, dev, rank, world):
             mix = fl["valu_mix_wave_instructions"]
             per_rs = lambda v: v * 64.0 / (fl["pmc_sample_rays"] * S14)       # wave-instructions -> per ray-surface
             issue_s = fl["issue_simd_cycles_per_ray"] * rays0 / SIMDS / PEAK_CLOCK_HZ
-            rl.update(achieved=fl["flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
-                      flops_per_ray=fl["flops_per_ray"], flops_kind=fl["flops_kind"],
+            rl.update(achieved=fl["executed_flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
                       executed_flops_per_ray=fl["executed_flops_per_ray"],
-                      achieved_executed=fl["executed_flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
+                      achieved_effective=fl["flops_per_ray"] * rays0 / (g[0][1] * 1e-3) / 1e12,
+                      effective_flops_per_ray=fl["flops_per_ray"], effective_flops_kind=fl["flops_kind"],
                       f64_wave_instructions_sample=fl["f64_wave_instructions"],
                       pmc_sample_rays=fl["pmc_sample_rays"],
-                      flops_method="algorithmic FLOPs per ray: PMC SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes "
-                                   "(FMA = 2) of a 1-field sweep at ONE wavelength, where every ray is traced alone, "
-                                   "scaled per ray (the analogue of algorithmic vs physical bytes); "
-                                   "executed_flops_per_ray: the same counters on the 1-field x 7-wavelength sample, "
-                                   "where the bundle rows share each ray's generation and first surface between a "
-                                   "field point's wavelengths; frac_issue: how close the kernel runs to its "
+                      flops_method="achieved / frac: the float64 FLOPs the kernel EXECUTES -- PMC "
+                                   "SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes (FMA = 2) on a 1-field x "
+                                   "7-wavelength sample, scaled per ray (a hardware-utilisation figure); "
+                                   "achieved_effective / frac_effective: the algorithmic FLOPs of a ray traced alone "
+                                   "(the same counters on a 1-field sweep at ONE wavelength), which the bundle rows "
+                                   "do not all execute -- they share each ray's generation and first surface between "
+                                   "a field point's wavelengths; frac_issue: how close the kernel runs to its "
                                    "instruction-issue ceiling",
                       valu_per_ray_surface=per_rs(mix["SQ_INSTS_VALU"]),
                       valu_mix_per_ray_surface={
@@ -699,6 +743,7 @@ def run_c5(args, dev, rank, world):
                                     "4) and a float64 transcendental at 2.97x (tools/valu/valu_rates.hip), over 1024 "
                                     "SIMDs at 2.4 GHz; frac_issue = that ceiling / the measured kernel time"))
             rl["frac"] = rl["achieved"] / F64_VALU_PEAK_TFLOPS
+            rl["frac_effective"] = rl["achieved_effective"] / F64_VALU_PEAK_TFLOPS
         else:
             rl["flops_note"] = err
     res["roofline"] = rl

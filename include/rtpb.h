@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 7   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+#define RTPB_ABI_VERSION 8   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
                                 3: input element type separate from the storage type (in_dtype)
                                 4: + rtpb_trace_checked (table-miss flag)
                                 5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers)
@@ -48,7 +48,11 @@ extern "C" {
                                 7: + rtpb_torch_alloc / rtpb_torch_free (torch MemPool segments),
                                    rtpb_buffer_stats; releasing a mapping synchronises the device;
                                    + rtpb_ray_fan_tables_wl / rtpb_collimated_rays_tables_wl (per-ray
-                                   wavelengths) */
+                                   wavelengths)
+                                8: + rtpb_trace_f64 / rtpb_trace_f32 (one-shot calls),
+                                   rtpb_oneshot_plans / rtpb_oneshot_clear; freeing a library buffer
+                                   never synchronises the device (retired mappings are released by the
+                                   next allocation that maps new memory, or by rtpb_buffer_trim) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -139,10 +143,12 @@ int rtpb_shutdown(void);
        those events on the device (hipStreamWaitEvent): nothing the new owner queues can touch the memory
        before the previous owner's recorded uses have finished.
    The pool keeps the most recently freed buffer per device (rtpb_set_tuning("buffer_pool_buffers", k)
-   keeps k, 0 none); an older one is unmapped and its physical memory released once its events have
-   completed (checked without blocking on later calls); its virtual range stays reserved, never reused.  rtpb_buffer_trim -- and
-   rtpb_shutdown, and an allocation that finds the device full -- waits for those events and releases
-   every pooled buffer.  rtpb_buffer_held reports the bytes and buffers the pool still holds on `device`
+   keeps k, 0 none); an older one retires, still mapped.  Freeing and pooled allocations never block (ABI 8):
+   retired buffers are unmapped and their physical memory released by the next allocation that maps new
+   memory (after a device synchronisation; not while that allocation's stream is capturing a graph), by
+   rtpb_buffer_trim and by rtpb_shutdown; their virtual ranges stay reserved, never reused.  rtpb_buffer_trim
+   -- and rtpb_shutdown, and an allocation that finds the device full -- waits for the recorded uses and
+   releases every pooled and retired buffer.  rtpb_buffer_held reports the bytes and buffers the pool still holds on `device`
    (-1: all devices).
    rtpb_buffer_dlpack wraps the whole buffer as a C-contiguous DLPack (v0.8 DLManagedTensor, device type
    ROCm) tensor of `ndim` extents `shape` and element type `dtype` (RTPB_F64 / RTPB_F32); ownership passes
@@ -211,6 +217,32 @@ int rtpb_trace_checked(const rtpb_plan* plan, int32_t device,
                        int64_t in_field_stride, void* out, int32_t out_layout, int64_t out_plane_stride,
                        int64_t out_field_stride, uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream,
                        int32_t* table_miss);
+
+/* ---- one-shot calls (the replacement of RT:658-659 without a plan handle) ------- */
+/* The whole system in one call: `surfaces` (nsurf) and `materials` (nmat = nsurf + 1: initial material,
+   System.materials, final material -- RT:653-656) as for rtpb_plan_create, device buffers as for rtpb_trace.
+     rays_in  device pointer, n_rays x 8 AOS records of double (rtpb_trace_f64) / float (rtpb_trace_f32)
+     out      device pointer: the history in the same element type (float: the float64 trace rounded once
+              on store, float rays widened exactly -- as rtpb_trace with an RTPB_F32 plan)
+     plane_mask_flags  0 = every plane 0..2S, (2S+1) x n_rays x 8 AOS: the reference's return value
+              (RT:1229-1232); RTPB_PLANES_FINAL = plane 2S alone (n_rays x 8); RTPB_OUT_SOA = planes stored
+              [8][n_rays] instead of [n_rays][8].  Other bits: RTPB_E_INVALID.  (Any other plane
+              selection: rtpb_plan_create + rtpb_trace.)
+   Asynchronous on `hip_stream` (NULL = the device's null stream).  The system is lowered into a plan once
+   and cached by content (every descriptor byte and the (wavelength, n) pairs of RTPB_TABLE materials; the
+   16 most recently used systems), so repeated calls with one system cost a compare of its descriptors.
+   rtpb_oneshot_plans returns the number of cached plans; rtpb_oneshot_clear drops them (a plan still in
+   use by a call on another thread is destroyed when that call returns; rtpb_shutdown clears them too). */
+#define RTPB_PLANES_FINAL 0x1u
+#define RTPB_OUT_SOA 0x2u
+int rtpb_trace_f64(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials, int32_t nmat,
+                   const double* rays_in, int64_t n_rays, double* out, uint32_t plane_mask_flags, int32_t device,
+                   void* hip_stream);
+int rtpb_trace_f32(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_material* materials, int32_t nmat,
+                   const float* rays_in, int64_t n_rays, float* out, uint32_t plane_mask_flags, int32_t device,
+                   void* hip_stream);
+int rtpb_oneshot_plans(void);
+void rtpb_oneshot_clear(void);
 
 /* ---- tracing host buffers (NumPy in, NumPy out), sharded over several GPUs ------------------ */
 /* rays_in: host, n_rays x 8 AOS of `in_dtype`.  out: host, nslots x n_rays x 8 AOS of the plan's dtype

@@ -11,13 +11,14 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 7
+RTPB_ABI_VERSION = 8
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
 RTPB_FLAT, RTPB_SPHERE, RTPB_PLANE_MIRROR, RTPB_PERFECT_LENS = 0, 1, 2, 3
 RTPB_CONSTANT, RTPB_SELLMEIER, RTPB_POLY6, RTPB_TABLE = 0, 1, 2, 3
 RTPB_MAX_SURFACES = 63
+RTPB_PLANES_FINAL, RTPB_OUT_SOA = 0x1, 0x2          # plane_mask_flags of rtpb_trace_f64 / _f32
 RTPB_OK, RTPB_E_INVALID, RTPB_E_HIP, RTPB_E_NODEV, RTPB_E_LIMIT = 0, -1, -2, -3, -4
 
 _c3 = ctypes.c_double * 3
@@ -69,6 +70,12 @@ SIGNATURES = {
     "rtpb_trace": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P]),
     "rtpb_trace_checked": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P,
                                           _P]),
+    "rtpb_trace_f64": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _P, _i64, _P,
+                                      ctypes.c_uint32, _i32, _P]),
+    "rtpb_trace_f32": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _P, _i64, _P,
+                                      ctypes.c_uint32, _i32, _P]),
+    "rtpb_oneshot_plans": (ctypes.c_int, []),
+    "rtpb_oneshot_clear": (None, []),
     "rtpb_trace_host": (ctypes.c_int, [_P, _P, _i32, _i64, _P, _u64, _u64, ctypes.POINTER(_i32), _i32]),
     "rtpb_ray_fan": (ctypes.c_int, [_i32, _i32, _P, ctypes.POINTER(_dbl), _dbl, _i64, _i64, ctypes.POINTER(_dbl),
                                     _dbl, _P]),

@@ -14,6 +14,7 @@ import collections
 import contextlib
 import ctypes
 import itertools
+import os
 import threading
 
 import numpy as np
@@ -94,6 +95,86 @@ def _lower_key(surfaces, materials, wl, dtype):
         return tuple(parts)
     except (TypeError, ValueError, AttributeError):
         return None
+
+
+# ------------------------------------------------------------------------- drop-in call memo
+# The content key above reads every lowered value on every trace (~10 us for the C2 system: a few % of a 1M-ray
+# trace).  A repeated call with the SAME surface list and material objects skips it when nothing can have changed:
+#   * MUTATIONS counts every attribute assignment or deletion on a Surface or a Material (their __setattr__ /
+#     __delattr__), so a radius, an aperture, a material coefficient or a whole array rebound since the memo was
+#     made invalidates it;
+#   * the lists are compared by element identity (a surface or a medium swapped);
+#   * arrays edited in place (s.center[2] = z) are caught by comparing the bytes of every array the lowering reads.
+# Only systems whose lowered values live in the instances' __dict__ as plain numbers and numeric arrays get a memo.
+MUTATIONS = [0]
+_CALLS = collections.OrderedDict()       # id(surfaces list) -> _Call
+_CALLS_MAX = 16
+
+
+class _Call:
+    __slots__ = ("surfaces", "items", "materials", "dtype", "gen", "arrays", "blob", "low")
+
+
+_SCALAR_ATTRS = ("aperture_rad", "radius", "focal_len", "alpha")
+_NUMBER = (int, float, np.floating, np.integer)
+
+
+def _call_arrays(surfaces):
+    """The arrays the lowering reads (center, input_axis, normal), or None when some lowered value is not held in
+    the instance's __dict__ as a numeric array or a plain number (properties, object arrays, lists)."""
+    arrs = []
+    for s in surfaces:
+        d = getattr(s, "__dict__", None)
+        if d is None:
+            return None
+        for name in ("center", "input_axis", "normal"):
+            a = d.get(name)
+            if a is None:
+                if name == "normal" and not hasattr(s, "normal"):
+                    continue
+                return None
+            if type(a) is not np.ndarray or a.dtype.kind not in "fiu":
+                return None
+            arrs.append(a)
+        for name in _SCALAR_ATTRS:
+            if name in d:
+                if not isinstance(d[name], _NUMBER):
+                    return None
+            elif hasattr(s, name):
+                return None
+    return arrs
+
+
+def memo_lookup(surfaces, materials, dtype):
+    """The lowering of the previous call with these very surface and material objects, if provably unchanged."""
+    e = _CALLS.get(id(surfaces))
+    if e is None or e.surfaces is not surfaces or e.gen != MUTATIONS[0] or e.dtype != dtype:
+        return None
+    if e.items != surfaces or e.materials != materials:
+        return None
+    if b"".join([a.tobytes() for a in e.arrays]) != e.blob:
+        return None
+    return e.low
+
+
+def memo_store(surfaces, materials, dtype, low):
+    """Remember ``low`` as the lowering of (surfaces, materials, dtype) for memo_lookup (untabulated systems)."""
+    if not isinstance(surfaces, list):
+        return
+    arrs = _call_arrays(surfaces)
+    if arrs is None:
+        return
+    for m in materials:
+        if not all(isinstance(v, _NUMBER) for v in vars(m).values() if v is not None and not isinstance(v, str)):
+            return
+    e = _Call()
+    e.surfaces, e.items, e.materials, e.dtype = surfaces, list(surfaces), list(materials), dtype
+    e.gen, e.arrays, e.blob, e.low = MUTATIONS[0], arrs, b"".join([a.tobytes() for a in arrs]), low
+    with _memo_lock:
+        _CALLS[id(surfaces)] = e
+        _CALLS.move_to_end(id(surfaces))
+        while len(_CALLS) > _CALLS_MAX:
+            _CALLS.popitem(last=False)
 
 
 def _pure_n(m):
@@ -378,13 +459,24 @@ def plan_for(low):
 
 
 def plane_mask(planes):
-    lo = hi = 0
-    for p in planes:
-        if p < 64:
-            lo |= 1 << p
-        else:
-            hi |= 1 << (p - 64)
-    return lo, hi
+    """(lo, hi) 64-bit halves of the 128-bit plane mask of rtpb_trace (memoised per plane list)."""
+    key = tuple(planes)
+    m = _MASKS.get(key)
+    if m is None:
+        lo = hi = 0
+        for p in key:
+            if p < 64:
+                lo |= 1 << p
+            else:
+                hi |= 1 << (p - 64)
+        m = _MASKS[key] = (lo, hi)
+        if len(_MASKS) > 256:
+            _MASKS.clear()
+            _MASKS[key] = m
+    return m
+
+
+_MASKS = {}
 
 
 def resolve_planes(planes, nsurf):
@@ -542,7 +634,56 @@ def history_buffer(shape, dtype, device, chunk_bytes=0, stream=None):
 _LIB_BUFFERS_USED = False
 _POOLS = {}
 _ALLOCATORS = {}            # a MemPool holds a raw pointer to its allocator: allocators live as long as the process
+_POOL_IDS = {}              # MemPool.id of each live pool (a property call per use otherwise)
 _pools_lock = threading.Lock()
+
+
+def hip_runtimes():
+    """The distinct files mapped into this process as a HIP runtime (libamdhip64*), from /proc/self/maps."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split(None, 5)[-1].strip()))
+    except OSError:
+        pass
+    return sorted(paths)
+
+
+def torch_hip_runtime():
+    """Directory of the HIP runtime torch ships (torch/lib): the one runtime librtpb must bind to."""
+    import torch
+    return os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib"))
+
+
+def check_one_hip_runtime():
+    """Raise unless exactly one HIP runtime is mapped and it is torch's: a second libamdhip64 (e.g. librtpb.so
+    loaded before torch, binding /opt/rocm's) would give librtpb its own device context, and pointers it maps for
+    torch's caching allocator would be foreign to torch's runtime."""
+    paths = hip_runtimes()
+    lib_dir = torch_hip_runtime()
+    if len(paths) != 1 or os.path.dirname(paths[0]) != lib_dir:
+        raise RuntimeError(f"history pool: expected one HIP runtime, torch's ({lib_dir}), mapped in this process; "
+                           f"found {paths}")
+
+
+def pool_allocator(device_index):
+    """The CUDAPluggableAllocator of device ``device_index``'s history pool (rtpb_torch_alloc / rtpb_torch_free),
+    created once and held for the life of the process.  Holding it is what keeps the pool valid: a MemPool keeps
+    only a raw pointer to its allocator's C++ object (torch._C._MemPool takes the allocator by pointer and does not
+    keep the Python object alive), so a pool whose allocator had been collected would call through freed memory at
+    its first allocation -- the segfault of round 5's first probe."""
+    import torch
+    idx = int(device_index)
+    alloc = _ALLOCATORS.get(idx)
+    if alloc is None:
+        C.lib()                 # loaded after torch: librtpb binds to torch's HIP runtime
+        check_one_hip_runtime()
+        alloc = _ALLOCATORS[idx] = torch.cuda.memory.CUDAPluggableAllocator(C.LIB_PATH, "rtpb_torch_alloc",
+                                                                            "rtpb_torch_free")
+        check_one_hip_runtime()
+    return alloc
 
 
 def history_pool(device_index):
@@ -550,36 +691,64 @@ def history_pool(device_index):
     librtpb's shuffled-chunk mappings as its segment allocator (rtpb_torch_alloc / rtpb_torch_free, ABI 7).
     torch owns everything else -- caching, stream-ordered reuse (Tensor.record_stream), memory statistics and
     out-of-memory handling; ``use_on_oom``: an allocation outside the pool that runs out of memory may take
-    the pool's cached blocks.  The pool's cached segments are released by :func:`trim_history_buffers` (a live
+    the pool's cached blocks.  The pool's unused segments are released by :func:`trim_history_buffers` (a live
     MemPool keeps them through torch.cuda.empty_cache())."""
     import torch
     idx = int(device_index)
     with _pools_lock:
         pool = _POOLS.get(idx)
         if pool is None:
-            alloc = _ALLOCATORS.get(idx)
-            if alloc is None:
-                C.lib()                 # loaded after torch: the allocator binds to torch's HIP runtime
-                alloc = _ALLOCATORS[idx] = torch.cuda.memory.CUDAPluggableAllocator(C.LIB_PATH, "rtpb_torch_alloc",
-                                                                                    "rtpb_torch_free")
+            alloc = pool_allocator(idx)
             with torch.cuda.device(idx):
                 pool = torch.cuda.MemPool(alloc.allocator(), use_on_oom=True)
             _POOLS[idx] = pool
+            _POOL_IDS[idx] = pool.id
     return pool
 
 
 def pool_empty(shape, dtype, device, stream=None):
     """torch.empty(shape, dtype, device) allocated in the device's history pool (:func:`history_pool`) for
-    ``stream`` (default: the current stream)."""
+    ``stream`` (default: the current stream).  torch.cuda.use_mem_pool's calls, made directly (the context
+    manager costs a few microseconds of the drop-in call)."""
     import torch
-    dev = torch.device(device)
+    dev = device if type(device) is torch.device else torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    pool = history_pool(idx)
+    pool = _POOLS.get(idx)
+    if pool is None:
+        pool = history_pool(idx)
+    pid = _POOL_IDS[idx]
     dev_ctx = torch.cuda.device(idx) if idx != torch.cuda.current_device() else contextlib.nullcontext()
     with dev_ctx:
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
-        with ctx, torch.cuda.use_mem_pool(pool, idx):
-            return torch.empty(shape, dtype=dtype, device=dev if dev.index is not None else torch.device("cuda", idx))
+        with ctx:
+            _begin_pool(idx, pid)
+            try:
+                return torch.empty(shape, dtype=dtype, device=dev if dev.index is not None else torch.device("cuda", idx))
+            finally:
+                _end_pool(idx, pid)
+                _release_pool(idx, pid)
+
+
+def _pool_calls():
+    """torch.cuda.use_mem_pool's three calls (torch 2.10: torch._C._cuda_beginAllocateCurrentThreadToPool,
+    _cuda_endAllocateToPool, _cuda_releasePool)."""
+    import torch
+    return (torch._C._cuda_beginAllocateCurrentThreadToPool, torch._C._cuda_endAllocateToPool,
+            torch._C._cuda_releasePool)
+
+
+def _begin_pool(idx, pid):
+    global _begin_pool, _end_pool, _release_pool
+    _begin_pool, _end_pool, _release_pool = _pool_calls()
+    _begin_pool(idx, pid)
+
+
+def _end_pool(idx, pid):            # replaced by _begin_pool's first call
+    _pool_calls()[1](idx, pid)
+
+
+def _release_pool(idx, pid):        # replaced by _begin_pool's first call
+    _pool_calls()[2](idx, pid)
 
 
 def buffer_stats(device=-1):
@@ -626,14 +795,19 @@ def history_buffers_held(device=-1):
 
 
 def trim_history_buffers():
-    """Release the device memory history buffers hold while unused: every history pool is dropped (torch then
-    returns its unused segments at once -- librtpb unmaps them -- and the rest when their tensors die; the next
-    history gets a new pool), and the library's own pool is emptied (rtpb_buffer_trim waits for the last
-    recorded uses)."""
+    """Release the device memory history buffers hold while unused.  A history pool none of whose blocks is in
+    use is dropped -- torch returns its segments at once (librtpb unmaps them) and the next history gets a new
+    pool.  A pool with live tensors is kept: dropping it would leave their blocks in an orphaned pool whose
+    memory nothing here counts or releases when they die; its cached blocks stay available to any
+    torch allocation that runs out of memory (use_on_oom), and a later trim releases the pool once its tensors are
+    gone.  The library's own pool is emptied too (rtpb_buffer_trim waits for the last recorded uses)."""
     with _pools_lock:
-        pools = list(_POOLS.values())
-        _POOLS.clear()
-    del pools
+        drop = []
+        for idx, pool in list(_POOLS.items()):
+            if all(int(seg["allocated_size"]) == 0 for seg in pool.snapshot()):
+                drop.append(_POOLS.pop(idx))
+                _POOL_IDS.pop(idx, None)
+    del drop
     C.check(C.lib().rtpb_buffer_trim())
 
 
@@ -661,10 +835,12 @@ def check_out(out, shape, dtype, device):
     return out
 
 
-def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None, miss=None):
+def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None, miss=None, own_out=False):
     """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA] of the
     plan's storage type.  ``miss``: a zeroed int32 CUDA tensor the launch sets to 1 when a ray's
-    wavelength is not a key of the plan's TABLE materials (rtpb_trace_checked)."""
+    wavelength is not a key of the plan's TABLE materials (rtpb_trace_checked).  ``stream``: None (torch's
+    current stream), a torch.cuda.Stream or a raw hipStream_t.  ``own_out``: ``out`` was just allocated by the
+    caller on the current stream (its use there needs no record)."""
     import torch
     tdt = torch.float64 if low.dtype == C.RTPB_F64 else torch.float32
     in_code = input_code(rays.dtype)
@@ -672,29 +848,39 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     if rays.dtype != want or not rays.is_contiguous():
         rays = rays.to(dtype=want).contiguous()
     n = rays.shape[0]
+    fresh_out = (out is None or own_out) and stream is None
     if out is None:
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
         out = device_empty(shape, tdt, rays.device)
     lo, hi = plane_mask(planes)
-    cur = None
     if stream is None:
         cur = torch.cuda.current_stream(rays.device)
         stream = cur.cuda_stream
+    elif isinstance(stream, torch.cuda.Stream):
+        cur, stream = stream, stream.cuda_stream
+    else:
+        # a raw hipStream_t: torch's view of it, so the launch's use can be recorded
+        cur = torch.cuda.ExternalStream(stream, device=rays.device)
     lib = C.lib()
-    with plan_ref(low) as plan:
+    p = _acquire(low)
+    try:
         if miss is None:
-            C.check(lib.rtpb_trace(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
-                                   out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream))
+            rc = lib.rtpb_trace(p.ptr, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
+                                out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream)
         else:
-            C.check(lib.rtpb_trace_checked(plan, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
-                                           0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr()))
+            rc = lib.rtpb_trace_checked(p.ptr, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
+                                        0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr())
+    finally:
+        _release(p)
+    if rc:
+        C.check(rc)
     if n:
         # the launch's use of `out` and of the rays on this stream, recorded: torch's allocator (a no-op on the
         # tensor's own stream) and the library's own buffer pool then hand the memory to a later owner only after
-        # this launch
-        if cur is not None:
+        # this launch.  (A history this call allocated itself lies on the launch stream already: no record.)
+        if not fresh_out:
             out.record_stream(cur)
-            rays.record_stream(cur)
+        rays.record_stream(cur)
         if _LIB_BUFFERS_USED:
             lib.rtpb_buffer_record_stream(out.data_ptr(), stream)
             lib.rtpb_buffer_record_stream(rays.data_ptr(), stream)

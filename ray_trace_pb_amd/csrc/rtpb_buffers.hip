@@ -21,17 +21,19 @@
 //     takes it and makes ITS stream wait (hipStreamWaitEvent, on the device) for those events, so no kernel
 //     of the new owner can touch the memory before the previous owner's last recorded use has finished;
 //   * the pool keeps only the most recently freed buffer per device (rtpb_set_tuning("buffer_pool_buffers")
-//     sets k, 0 = none); older ones retire: each is unmapped and its physical memory released (its virtual
-//     range kept reserved) once its events have completed -- checked without blocking on every
-//     later alloc / free, and waited for by rtpb_buffer_trim, rtpb_shutdown and an allocation that finds the
-//     device full.
+//     sets k, 0 = none); older ones retire.  A retired buffer stays mapped until a call that may block
+//     releases it: the next allocation that maps new memory (rtpb_buffer_alloc without a pooled match, or a
+//     torch segment, rtpb_torch_alloc -- not while its stream is capturing a graph), rtpb_buffer_trim,
+//     rtpb_shutdown.  Those synchronise the device and unmap every retired buffer; a free, a pooled
+//     allocation and rtpb_buffer_held never block (ABI 8: a free inside a DLPack deleter, i.e. a Python
+//     tensor's destructor, can run during stream capture).
 //
 // torch's own caching allocator can use the same memory (ABI 7): rtpb_torch_alloc / rtpb_torch_free are the
 // allocation functions of a torch.cuda.memory.CUDAPluggableAllocator behind a torch.cuda.MemPool
 // (ray_trace_pb_amd._engine.history_pool).  torch then owns streams, caching, record_stream, statistics and
 // out-of-memory handling of those segments; the library only maps (alloc) and unmaps (free) them.
 //
-// Releasing a mapping always synchronises the device first: torch frees without a device sync, and a use on a
+// Releasing a mapping always follows a device synchronisation: torch frees without a device sync, and a use on a
 // stream never recorded may still be in flight (HIP's unmap, unlike hipFree, does not wait for it).  The
 // virtual range of a buffer a kernel may have used is kept reserved (a range freed and reserved
 // again took writes through its old translations in round 4); those dead ranges are counted
@@ -78,29 +80,23 @@ int stream_device(hipStream_t s, int fallback) {
     return d;
 }
 
-bool events_done(const Buffer* b) {
-    for (hipEvent_t e : b->pending)
-        if (hipEventQuery(e) != hipSuccess) return false;
-    return true;
-}
-
 void drop_events(Buffer* b) {
     for (hipEvent_t e : b->pending) (void)hipEventDestroy(e);
     b->pending.clear();
 }
 
 // Unmaps and releases the physical chunks of a buffer, after waiting for the recorded uses of its last owner
-// (b->pending) and for the whole device: a use on a stream nobody recorded may still be in flight, and an
-// unmap does not wait for it.  `used`: a kernel may have touched the memory -- its virtual range then stays
-// reserved (counted in g_dead_va); a buffer no kernel saw (an allocation that failed half way) frees it.
-// The Buffer object is deleted.
-int destroy(Buffer* b, bool used = true) {
+// (b->pending) and -- unless the caller has just done so (`synced`) -- for the whole device: a use on a stream
+// nobody recorded may still be in flight, and an unmap does not wait for it.  `used`: a kernel may have touched
+// the memory -- its virtual range then stays reserved (counted in g_dead_va); a buffer no kernel saw (an
+// allocation that failed half way) frees it.  The Buffer object is deleted.
+int destroy(Buffer* b, bool used = true, bool synced = false) {
     DeviceGuard g(b->dev);
     hipError_t e = hipSuccess;
     for (hipEvent_t ev : b->pending)
         if (hipEventSynchronize(ev) != hipSuccess) e = hipErrorUnknown;
     drop_events(b);
-    if (used && hipDeviceSynchronize() != hipSuccess) e = hipErrorUnknown;
+    if (used && !synced && hipDeviceSynchronize() != hipSuccess) e = hipErrorUnknown;
     if (b->plain) {
         if (b->va && hipFree(b->va) != hipSuccess) e = hipErrorUnknown;
     } else {
@@ -124,25 +120,37 @@ int destroy(Buffer* b, bool used = true) {
     return e == hipSuccess ? RTPB_OK : fail(RTPB_E_HIP, "rtpb_buffer: releasing a mapping failed");
 }
 
-// Retired buffers whose last uses have completed (never blocks); caller holds g_mu.
-std::vector<Buffer*> collect_retired_locked() {
-    std::vector<Buffer*> done;
-    for (size_t k = 0; k < g_retired.size();) {
-        if (events_done(g_retired[k])) {
-            done.push_back(g_retired[k]);
-            g_retired.erase(g_retired.begin() + static_cast<std::ptrdiff_t>(k));
-        } else {
-            ++k;
-        }
-    }
-    return done;
-}
-
+// Destroys `v`: one device synchronisation per device involved, then every unmap.
 int destroy_all(const std::vector<Buffer*>& v) {
     int rc = RTPB_OK;
+    std::vector<int> synced;
+    for (Buffer* b : v) {
+        if (std::find(synced.begin(), synced.end(), b->dev) != synced.end()) continue;
+        DeviceGuard g(b->dev);
+        if (hipDeviceSynchronize() != hipSuccess) rc = RTPB_E_HIP;
+        synced.push_back(b->dev);
+    }
     for (Buffer* b : v)
-        if (destroy(b) != RTPB_OK) rc = RTPB_E_HIP;
+        if (destroy(b, true, true) != RTPB_OK) rc = RTPB_E_HIP;
     return rc;
+}
+
+// Every retired buffer (a blocking point: the device is synchronised before the unmaps).  Not while `stream`
+// captures a graph -- a device synchronisation would invalidate the capture; the buffers wait for a later call.
+int release_retired(hipStream_t stream) {
+    if (stream != nullptr) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            return RTPB_OK;
+        }
+    }
+    std::vector<Buffer*> all;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        all.swap(g_retired);
+    }
+    return destroy_all(all);
 }
 
 // The owner's last use on each stream it used, as events (the free itself never waits).
@@ -173,7 +181,6 @@ int record_pending(Buffer* b) {
 // Back to the pool (newest last); beyond g_pool_keep per device the oldest pooled buffers retire.
 int release(Buffer* b) {
     int rc = record_pending(b);
-    std::vector<Buffer*> done;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         g_live.erase(reinterpret_cast<uintptr_t>(b->va));
@@ -190,16 +197,13 @@ int release(Buffer* b) {
                 ++k;
             }
         }
-        done = collect_retired_locked();
     }
-    if (destroy_all(done) != RTPB_OK) rc = RTPB_E_HIP;
     return rc;
 }
 
 // A pooled buffer of this size for `stream`: the stream waits (on the device) for the previous owner's uses.
 Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk, hipStream_t stream) {
     Buffer* b = nullptr;
-    std::vector<Buffer*> done;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         for (size_t k = g_pool.size(); k-- > 0;) {
@@ -210,9 +214,7 @@ Buffer* take_pooled(int dev, uint64_t size, uint64_t chunk, hipStream_t stream) 
                 break;
             }
         }
-        done = collect_retired_locked();
     }
-    (void)destroy_all(done);
     if (!b) return nullptr;
     for (hipEvent_t ev : b->pending) {
         if (hipEventQuery(ev) == hipSuccess) continue;
@@ -338,13 +340,14 @@ int chunk_geometry(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_
 
 // A new buffer of at least `bytes` on `device`: physical chunks mapped in a shuffled order into a fresh
 // virtual range -- or, once the dead virtual ranges exceed g_dead_va_limit, one plain hipMalloc allocation.
-// Out of device memory, the library's pooled and retired buffers of the device are released once and the
-// allocation retried.
-int map_new(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, Buffer** out) {
+// Retired buffers are released first (release_retired: unless `stream` is capturing).  Out of device memory,
+// the library's pooled and retired buffers of the device are released once and the allocation retried.
+int map_new(int32_t device, uint64_t bytes, uint64_t chunk_bytes, uint64_t seed, hipStream_t stream, Buffer** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return fail(RTPB_E_NODEV, "rtpb_buffer_alloc: no such device");
     DeviceGuard g(device);
+    (void)release_retired(stream);
     const hipMemAllocationProp prop = device_prop(device);
     uint64_t chunk = 0, n = 0, gran = 1;
     const int rc = chunk_geometry(device, bytes, chunk_bytes, &chunk, &n, &gran);
@@ -434,7 +437,7 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
         }
     }
     Buffer* b = nullptr;
-    const int rc = map_new(device, bytes, chunk_bytes, seed, &b);
+    const int rc = map_new(device, bytes, chunk_bytes, seed, st, &b);
     if (rc != RTPB_OK) return rc;
     own(b, st);
     *ptr = b->va;
@@ -446,10 +449,11 @@ extern "C" int rtpb_buffer_alloc(int32_t device, uint64_t bytes, uint64_t chunk_
 // torch MemPool -- a fresh shuffled-chunk mapping (torch's caching allocator caches and reuses it).  NULL on
 // failure (torch then frees its cached blocks and retries, or raises its out-of-memory error).
 extern "C" void* rtpb_torch_alloc(int64_t size, int32_t device, void* stream) {
-    (void)stream;
     if (size <= 0) return nullptr;
     Buffer* b = nullptr;
-    if (map_new(device, static_cast<uint64_t>(size), 0, g_torch_seed.fetch_add(1), &b) != RTPB_OK) return nullptr;
+    if (map_new(device, static_cast<uint64_t>(size), 0, g_torch_seed.fetch_add(1), static_cast<hipStream_t>(stream),
+                &b) != RTPB_OK)
+        return nullptr;
     std::lock_guard<std::mutex> lk(g_mu);
     g_torch[reinterpret_cast<uintptr_t>(b->va)] = b;
     ++g_torch_allocs;
@@ -516,10 +520,8 @@ extern "C" int rtpb_buffer_held(int32_t device, uint64_t* bytes, int32_t* buffer
     if (!bytes || !buffers) return fail(RTPB_E_INVALID, "rtpb_buffer_held: null output");
     uint64_t tot = 0;
     int32_t cnt = 0;
-    std::vector<Buffer*> done;
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        done = collect_retired_locked();
         for (auto* list : {&g_pool, &g_retired})
             for (Buffer* b : *list)
                 if (device < 0 || b->dev == device) {
@@ -529,7 +531,7 @@ extern "C" int rtpb_buffer_held(int32_t device, uint64_t* bytes, int32_t* buffer
     }
     *bytes = tot;
     *buffers = cnt;
-    return destroy_all(done);
+    return RTPB_OK;
 }
 
 extern "C" int rtpb_buffer_dlpack(void* handle, int32_t ndim, const int64_t* shape, int32_t dtype, void** managed) {

@@ -223,6 +223,7 @@ int host_shard_pipeline(rtpb_plan* plan, int dev, const char* in, int in_dtype, 
 extern "C" {
 
 int rtpb_shutdown(void) {
+    rtpb_oneshot_clear();                          // the one-shot entry points' cached plans (rtpb_oneshot.hip)
     (void)rtpb_buffer_trim();                      // pooled history buffers (rtpb_buffers.hip)
     for (int d = 0; d < kMaxDevices; ++d) {
         HostStage& hs = g_stage[d];

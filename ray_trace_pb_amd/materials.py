@@ -17,6 +17,8 @@ descriptor each material lowers to (:meth:`Material._rtpb_lower`):
 """
 import numpy as np
 
+from . import _engine as _E
+
 # (b1, b2, b3), (c1, c2, c3) Sellmeier coefficients, wavelength in um (Schott / refractiveindex.info)
 _SELLMEIER = {
     "FusedSilica": ((0.6961663, 0.4079426, 0.8974794), (0.0684043 ** 2, 0.1162414 ** 2, 9.896161 ** 2)),
@@ -51,6 +53,16 @@ class Material:
     wf = 0.4861   # hydrogen F-line
     wc = 0.6563   # hydrogen C-line
     vd = None
+
+    # every assignment / deletion of an attribute is counted: the drop-in call's lowering memo is valid only while
+    # the count is unchanged (_engine.memo_lookup)
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        _E.MUTATIONS[0] += 1
+
+    def __delattr__(self, name):
+        object.__delattr__(self, name)
+        _E.MUTATIONS[0] += 1
 
     def __init__(self, b_coeffs, c_coeffs):
         self.b1, self.b2, self.b3 = np.array(b_coeffs).squeeze()

@@ -474,21 +474,25 @@ def trace_surfaces(surfaces, materials, rays, *, planes="all", dtype=None, devic
         return _trace_segmented(surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices, layout=layout)
     if not on_device:
         rays = np.asarray(rays)
-    if rays.ndim == 1:
+    nd = rays.ndim
+    if nd == 2:
+        last = rays                     # the common (N, 8) bundle: no views (a torch view costs microseconds)
+    elif nd == 1:
         rays = rays[None, None, :]
-    elif rays.ndim == 2:
-        rays = rays[None]
-    if rays.ndim != 3 or rays.shape[-1] != 8:
+        last = rays[-1]
+    elif nd == 3:
+        last = rays[-1]
+    if nd not in (1, 2, 3) or rays.shape[-1] != 8:
         raise ValueError(f"rays must have shape (8,), (N, 8) or (k, N, 8); got {tuple(rays.shape)}")
-    k, n = rays.shape[0], rays.shape[1]
+    k = rays.shape[0] if nd == 3 else 1
+    n = last.shape[0]
     code = _dtype_code(dtype, rays)
     sel = E.resolve_planes(planes, len(surfaces))
-    full = isinstance(planes, str) and planes == "all"
-    last = rays[-1]
+    full = planes == "all" if isinstance(planes, str) else False
 
     layout_code = C.RTPB_AOS if layout == "aos" else C.RTPB_SOA
     if on_device:
-        return _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out)
+        return _trace_device_tables(surfaces, materials, rays, last, code, sel, full and k > 1, layout_code, out)
 
     def wavelengths():
         return E.distinct_wavelengths(last[:, 7])
@@ -542,29 +546,36 @@ def _miss_flag(device):
     return f
 
 
-def _trace_device_tables(surfaces, materials, rays, last, code, sel, full, layout_code, out=None):
+def _trace_device_tables(surfaces, materials, rays, last, code, sel, extend, layout_code, out=None):
     """The torch-CUDA trace of trace_surfaces.  Tabulated materials (user n() overrides, Ebaf11) are
     lowered with the key set of the previous bundle traced through them when there is one, and the kernel
     flags any ray whose wavelength is not among those keys (rtpb_trace_checked); only then is the bundle's
     wavelength column scanned (rtpb_distinct_keys) and the bundle re-traced with its own keys.  Either
-    way every ray reads n() of its own wavelength: bit-identical to lowering with the bundle's keys."""
+    way every ray reads n() of its own wavelength: bit-identical to lowering with the bundle's keys.
+    ``extend``: ``rays`` is a (k > 1, N, 8) history that the full trace extends (RT:1175-1178)."""
     import torch
-    k = rays.shape[0]
     if out is not None:
         n = last.shape[0]
         shape = (len(sel), n, 8) if layout_code == C.RTPB_AOS else (len(sel), 8, n)
         E.check_out(out, shape, torch.float64 if code == C.RTPB_F64 else torch.float32, last.device)
 
     def run(low, miss=None):
-        if full and k > 1:
+        if extend:
             new = E.trace_device(low, last, sel[1:], miss=miss)
             return torch.cat((rays.to(new.dtype), new), dim=0)
-        dst = out if out is not None else _default_history(code, last, sel, layout_code)
-        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=dst)
+        if out is not None:
+            return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=out)
+        dst = _default_history(code, last, sel, layout_code)
+        return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=dst, own_out=dst is not None)
 
+    low = E.memo_lookup(surfaces, materials, code)
+    if low is not None:
+        return run(low)
     tab = E.tabulated(materials)
     if not tab:
-        return run(E.lower(surfaces, materials, None, code, tab=tab))
+        low = E.lower(surfaces, materials, None, code, tab=tab)
+        E.memo_store(surfaces, materials, code, low)
+        return run(low)
     fp = E.table_fingerprint(tab)
     prev = E.previous_keys(fp)
     if prev is not None:
@@ -749,6 +760,9 @@ def propagate_user_geometry(surface, ray_array, material1, material2, *, devices
     return np.concatenate((hist, new.cpu().numpy()), axis=0)
 
 
+_CUSTOM = {}       # tuple of surface classes -> per surface: runs its own propagate / geometry hooks (class properties)
+
+
 class System:
     """An ordered collection of optical surfaces with the materials between them (RT:359-932).
 
@@ -848,7 +862,10 @@ class System:
         materials = [initial_material] + list(self.materials) + [final_material]
         if len(materials) != len(self.surfaces) + 1:
             raise ValueError("length of materials should be len(surfaces) + 1")
-        custom = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
+        classes = tuple(map(type, self.surfaces))
+        custom = _CUSTOM.get(classes)
+        if custom is None:
+            custom = _CUSTOM[classes] = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,
                                   layout=layout, gather=gather, out=out)
@@ -1110,6 +1127,16 @@ def _surface_class_info(cls):
 
 class Surface:
     """Base optical surface: input/output axes, center, paraxial center, aperture radius (RT:1031-1156)."""
+
+    # every assignment / deletion of an attribute is counted: the drop-in call's lowering memo is valid only while
+    # the count is unchanged (_engine.memo_lookup)
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        E.MUTATIONS[0] += 1
+
+    def __delattr__(self, name):
+        object.__delattr__(self, name)
+        E.MUTATIONS[0] += 1
 
     def __init__(self, input_axis, output_axis, center, paraxial_center, aperture_rad: float):
         self.input_axis = np.array(input_axis).squeeze().astype(float)

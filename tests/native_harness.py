@@ -115,3 +115,20 @@ def build_vmm_check():
                     "-Wall", "-o", tmp, VMM_SRC], check=True)
     os.replace(tmp, VMM_OUT)
     return VMM_OUT
+
+
+VMM_LIB = os.path.join(HERE, "native", "_build", "libvmm_remap_check.so")
+
+
+def build_vmm_check_lib():
+    """The same check as a shared library (entry vmm_remap_check_run), for tools/vmm_torch_runtime.py: loaded after
+    torch it binds to torch's HIP runtime (one libamdhip64 per process, matched by SONAME), the runtime every
+    product process uses."""
+    if os.path.exists(VMM_LIB) and os.path.getmtime(VMM_LIB) >= os.path.getmtime(VMM_SRC):
+        return VMM_LIB
+    os.makedirs(os.path.dirname(VMM_LIB), exist_ok=True)
+    tmp = f"{VMM_LIB}.{os.getpid()}.tmp"
+    subprocess.run([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--offload-arch=gfx950", "-O2", "-std=c++17",
+                    "-Wall", "-shared", "-fPIC", "-o", tmp, VMM_SRC], check=True)
+    os.replace(tmp, VMM_LIB)
+    return VMM_LIB

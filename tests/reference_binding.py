@@ -54,6 +54,50 @@ def _builtin_kind(rt, s):
     return None
 
 
+def lower_surface(s, kind):
+    """rtpb_surface of a reference surface object of built-in ``kind`` (RT:1035-1069 attributes)."""
+    d = _Surf()
+    d.kind = kind
+    d.center[:] = np.asarray(s.center, dtype=float).ravel()
+    d.input_axis[:] = np.asarray(s.input_axis, dtype=float).ravel()
+    d.normal[:] = np.asarray(getattr(s, "normal", s.input_axis), dtype=float).ravel()
+    d.aperture = float(s.aperture_rad)
+    d.on_tol = 1e-12                                    # RT:1343, 1408, 1528
+    if kind == 1:
+        d.radius, d.radius_sq = float(s.radius), float(s.radius ** 2)          # RT:1499
+    if kind == 3:
+        d.focal_len, d.sin_alpha = float(s.focal_len), float(np.sin(s.alpha))  # RT:1758
+    return d
+
+
+def lower_material(mat, m, wl):
+    """rtpb_material of a reference material (``mat``: raytrace.materials); ``wl``: the bundle's distinct
+    wavelengths, the keys of a table for any n() the kernel does not evaluate itself."""
+    d = _Mat()
+    if type(m).n is mat.Constant.n:
+        d.kind, d.c[0] = 0, float(m._n)
+    elif type(m).n is mat.Material.n:                   # Sellmeier (MAT:39-51), Vacuum
+        d.kind = 1
+        d.c[:] = [float(v) for v in (m.b1, m.b2, m.b3, m.c1, m.c2, m.c3)]
+    else:                                               # Ebaf11 or a user n(): its own values
+        d._tab = np.ascontiguousarray(np.stack((wl, np.broadcast_to(np.asarray(m.n(wl), dtype=float), wl.shape)),
+                                               axis=1))
+        d.kind, d.table_len = 3, wl.size
+        d.table = d._tab.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    return d
+
+
+def lower_system(rt, mat, surfaces, materials, wl):
+    """(rtpb_surface array, rtpb_material array, keep-alive list) of built-in surfaces and their S+1 materials."""
+    kinds = [_builtin_kind(rt, s) for s in surfaces]
+    if any(k is None for k in kinds):
+        raise ValueError("user surface geometry: not lowerable")
+    S = len(surfaces)
+    surf = (_Surf * max(S, 1))(*[lower_surface(s, k) for s, k in zip(surfaces, kinds)])
+    keep = [lower_material(mat, m, wl) for m in materials]   # keeps the table arrays alive
+    return surf, (_Mat * (S + 1))(*keep), keep
+
+
 def make_ray_trace(rt, mat, lib_path):
     """System.ray_trace replacement bound to librtpb.so at ``lib_path`` (``rt`` / ``mat``: the
     reference's raytrace.raytrace / raytrace.materials modules)."""
@@ -66,39 +110,11 @@ def make_ray_trace(rt, mat, lib_path):
                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     python_loop = rt.System.ray_trace
 
-    def lower_surface(s, kind):
-        d = _Surf()
-        d.kind = kind
-        d.center[:] = np.asarray(s.center, dtype=float).ravel()
-        d.input_axis[:] = np.asarray(s.input_axis, dtype=float).ravel()
-        d.normal[:] = np.asarray(getattr(s, "normal", s.input_axis), dtype=float).ravel()
-        d.aperture = float(s.aperture_rad)
-        d.on_tol = 1e-12                                    # RT:1343, 1408, 1528
-        if kind == 1:
-            d.radius, d.radius_sq = float(s.radius), float(s.radius ** 2)          # RT:1499
-        if kind == 3:
-            d.focal_len, d.sin_alpha = float(s.focal_len), float(np.sin(s.alpha))  # RT:1758
-        return d
-
-    def lower_material(m, wl):
-        d = _Mat()
-        if type(m).n is mat.Constant.n:
-            d.kind, d.c[0] = 0, float(m._n)
-        elif type(m).n is mat.Material.n:                   # Sellmeier (MAT:39-51), Vacuum
-            d.kind = 1
-            d.c[:] = [float(v) for v in (m.b1, m.b2, m.b3, m.c1, m.c2, m.c3)]
-        else:                                               # Ebaf11 or a user n(): its own values
-            d._tab = np.ascontiguousarray(np.stack((wl, np.broadcast_to(np.asarray(m.n(wl), dtype=float), wl.shape)),
-                                                   axis=1))
-            d.kind, d.table_len = 3, wl.size
-            d.table = d._tab.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
-        return d
-
     def trace_segment(surfaces, kinds, materials, rays2d):
         S = len(surfaces)
         wl = np.unique(rays2d[:, 7])
         surf = (_Surf * S)(*[lower_surface(s, k) for s, k in zip(surfaces, kinds)])
-        keep = [lower_material(m, wl) for m in materials]   # keeps the table arrays alive
+        keep = [lower_material(mat, m, wl) for m in materials]   # keeps the table arrays alive
         mats = (_Mat * (S + 1))(*keep)
         plan = ctypes.c_void_p()
         if lib.rtpb_plan_create(surf, S, mats, S + 1, 0, ctypes.byref(plan)) != 0:
@@ -133,3 +149,17 @@ def make_ray_trace(rt, mat, lib_path):
         return hist
 
     return ray_trace
+
+
+def bind_oneshot(lib_path):
+    """The one-shot entry points (ABI 8) with their argument types: rtpb_trace_f64 /
+    rtpb_trace_f32(surfaces, nsurf, materials, nmat, rays_in, n, out, plane_mask_flags, device, hip_stream) on
+    device pointers -- e.g. CuPy's / torch's ``data_ptr()`` -- for a caller that keeps its rays on the GPU."""
+    lib = ctypes.CDLL(lib_path)
+    lib.rtpb_last_error.restype = ctypes.c_char_p
+    for name in ("rtpb_trace_f64", "rtpb_trace_f32"):
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.POINTER(_Surf), ctypes.c_int32, ctypes.POINTER(_Mat), ctypes.c_int32, ctypes.c_void_p,
+                       ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p]
+    return lib

@@ -287,3 +287,43 @@ def test_lowering_memo_follows_in_place_changes():
     assert d is not low0 and bytes(d.surfaces) != bytes(low0.surfaces)
     system.surfaces[-1].center[2] = z0
     assert E.lower(system.surfaces, mats, None, C.RTPB_F64) is low0
+
+
+def test_call_memo_follows_every_change():
+    """The drop-in call's memo (a repeated System.ray_trace skips the content key) returns the
+    previous lowering only while nothing it read can have changed: in-place array edits, attribute rebinding on a
+    surface or a material, a swapped surface or medium and another storage type each miss; undoing an in-place
+    edit hits again (the bytes match)."""
+    system = systems.c2_system(rt, mat)
+    m0, m1 = mat.Vacuum(), mat.Vacuum()
+
+    def mats():
+        return [m0] + list(system.materials) + [m1]
+    low = E.lower(system.surfaces, mats(), None, C.RTPB_F64)
+    E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F32) is None
+    z0 = system.surfaces[-1].center[2]
+    system.surfaces[-1].center[2] = z0 + 1.0                      # in place: the bytes differ
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    system.surfaces[-1].center[2] = z0
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    system.surfaces[-1].normal[2] = system.surfaces[-1].normal[2]     # an int64 normal array, unchanged bytes
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    sph = system.surfaces[1]
+    sph.radius = sph.radius                                          # any rebinding counts
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
+    m0.b1 = m0.b1                                                    # a material attribute
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
+    assert E.memo_lookup(system.surfaces, [mat.Vacuum()] + mats()[1:], C.RTPB_F64) is None   # another medium
+    old = system.surfaces[0]
+    system.surfaces[0] = rt.FlatSurface(old.center, old.normal, old.aperture_rad)            # another surface
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    system.surfaces[0] = old
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None    # (constructing a surface counted too)
+    E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    del sph.radius                                                   # deletion counts too
+    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None

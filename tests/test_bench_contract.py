@@ -83,3 +83,13 @@ def test_bench_gpus_n_without_gpus_fails_before_launching():
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_strong_scaling_fields():
+    """configs.c4 / configs.c5 of an N > 1 line carry their own t1 (rank 0 alone, same job) and efficiency
+    t1 / (N tN) (VERDICT r05 #5)."""
+    r = bench.strong_scaling(13.5, 1.8, 8)
+    assert r["t1_ms"] == 13.5 and r["tN_ms"] == 1.8
+    assert abs(r["speedup"] - 7.5) < 1e-12
+    assert abs(r["scaling_efficiency"] - 13.5 / (8 * 1.8)) < 1e-12
+    assert abs(bench.strong_scaling(10.0, 5.0, 2)["scaling_efficiency"] - 1.0) < 1e-12

@@ -92,6 +92,32 @@ def test_trace_without_gpu_fails_loudly():
     lib.rtpb_plan_destroy(plan)
 
 
+def test_oneshot_validates_arguments():
+    """rtpb_trace_f64 / _f32: bad flags, a material count other than S + 1 and a negative ray
+    count fail with RTPB_E_INVALID before any device work."""
+    lib = C.lib()
+    surf, mats = _flat_plan_args(2)
+    assert lib.rtpb_trace_f64(surf, 2, mats, 3, None, 0, None, 0x10, 0, None) == -1
+    assert b"plane_mask_flags" in lib.rtpb_last_error()
+    assert lib.rtpb_trace_f32(surf, 2, mats, 2, None, 0, None, 0, 0, None) == -1
+    assert b"len(surfaces) + 1" in lib.rtpb_last_error()
+    assert lib.rtpb_trace_f64(surf, 2, mats, 3, None, -1, None, 0, 0, None) == -1
+    assert lib.rtpb_trace_f64(surf, 64, mats, 65, None, 0, None, 0, 0, None) == -4
+
+
+@pytest.mark.skipif(C.device_count() > 0, reason="checks the no-GPU error path")
+def test_oneshot_without_gpu_fails_loudly():
+    lib = C.lib()
+    surf, mats = _flat_plan_args(1)
+    lib.rtpb_oneshot_clear()
+    rays = np.zeros((4, 8))
+    assert lib.rtpb_trace_f64(surf, 1, mats, 2, rays.ctypes.data, 4, rays.ctypes.data, 0, 0, None) == -3
+    assert b"no GPU" in lib.rtpb_last_error()
+    assert lib.rtpb_oneshot_plans() == 1            # the system was lowered and cached before the device check
+    lib.rtpb_oneshot_clear()
+    assert lib.rtpb_oneshot_plans() == 0
+
+
 @pytest.mark.skipif(C.device_count() > 0, reason="checks the no-GPU error path")
 def test_system_ray_trace_raises_without_gpu():
     import ray_trace_pb_amd.materials as mat

@@ -76,3 +76,65 @@ def test_binding_chains_launches_beyond_63_surfaces(ray_trace_gpu):
                       [material_to_dict(m) for m in [m0] + list(system.materials) + [m1]], rays)
     got = ray_trace_gpu(system, rays, m0, m1)
     assert got.shape == ref.shape and same_bits(got, ref)
+
+
+# ---- the one-shot entry points of SURVEY.md 8(b) (ABI 8): rtpb_trace_f64 / rtpb_trace_f32 on device buffers
+def _oneshot_case(name):
+    import torch
+    d = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    system, m0, m1 = system_from_json(rt, mat, str(d["system_json"]))
+    mats = [m0] + list(system.materials) + [m1]
+    surf, mtab, keep = reference_binding.lower_system(rt, mat, system.surfaces, mats, np.unique(d["rays_in"][:, 7]))
+    return d, system, mats, surf, mtab, keep, torch
+
+
+@pytest.mark.parametrize("name", ["c1_plano_convex", "c2_achromat", "c3_relay", "c4_opm"])
+def test_oneshot_f64_reproduces_reference_histories(name):
+    """rtpb_trace_f64 (every plane, AOS) on the C1-C4 goldens: the reference's float64 history bit for bit; the
+    final-plane and SOA flags give the same values; a second call hits the content-keyed plan cache."""
+    d, system, mats, surf, mtab, keep, torch = _oneshot_case(name)
+    lib = reference_binding.bind_oneshot(C.LIB_PATH)
+    S, n = len(system.surfaces), d["rays_in"].shape[0]
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(np.ascontiguousarray(d["rays_in"])).to(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    lib.rtpb_oneshot_clear()
+    out = torch.full((2 * S + 1, n, 8), 7.0, dtype=torch.float64, device=dev)
+    assert lib.rtpb_trace_f64(surf, S, mtab, S + 1, x.data_ptr(), n, out.data_ptr(), 0, 0, st) == 0
+    assert lib.rtpb_oneshot_plans() == 1
+    fin = torch.empty((n, 8), dtype=torch.float64, device=dev)
+    assert lib.rtpb_trace_f64(surf, S, mtab, S + 1, x.data_ptr(), n, fin.data_ptr(), C.RTPB_PLANES_FINAL, 0, st) == 0
+    soa = torch.empty((2 * S + 1, 8, n), dtype=torch.float64, device=dev)
+    assert lib.rtpb_trace_f64(surf, S, mtab, S + 1, x.data_ptr(), n, soa.data_ptr(), C.RTPB_OUT_SOA, 0, st) == 0
+    assert lib.rtpb_oneshot_plans() == 1                    # one system, one cached plan
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), d["history"])
+    assert same_bits(fin.cpu().numpy(), d["history"][-1])
+    assert same_bits(soa.transpose(1, 2).cpu().numpy(), d["history"])
+    assert lib.rtpb_trace_f64(surf, S, mtab, S + 1, x.data_ptr(), n, out.data_ptr(), 4, 0, st) == -1   # unknown flag
+    assert b"plane_mask_flags" in lib.rtpb_last_error()
+    lib.rtpb_oneshot_clear()
+    assert lib.rtpb_oneshot_plans() == 0
+
+
+@pytest.mark.parametrize("name", ["c1_plano_convex", "c2_achromat"])
+def test_oneshot_f32_is_the_float64_trace_rounded_once(name):
+    """rtpb_trace_f32 on float32 rays: the float64 trace of the widened rays (the oracle, bitwise against the
+    reference) rounded once to float32 -- as System.ray_trace(float32 rays, dtype='float32')."""
+    d, system, mats, surf, mtab, keep, torch = _oneshot_case(name)
+    from serialize import material_to_dict, surface_to_dict
+    lib = reference_binding.bind_oneshot(C.LIB_PATH)
+    S = len(system.surfaces)
+    rays32 = np.ascontiguousarray(d["rays_in"].astype(np.float32))
+    n = rays32.shape[0]
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(rays32).to(dev)
+    out = torch.empty((2 * S + 1, n, 8), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    assert lib.rtpb_trace_f32(surf, S, mtab, S + 1, x.data_ptr(), n, out.data_ptr(), 0, 0, st) == 0
+    torch.cuda.synchronize()
+    ref = O.ray_trace([surface_to_dict(s) for s in system.surfaces], [material_to_dict(m) for m in mats],
+                      rays32.astype(np.float64))
+    assert same_bits(out.cpu().numpy(), ref.astype(np.float32))
+    drop = system.ray_trace(x, mats[0], mats[-1], dtype="float32")
+    assert same_bits(out.cpu().numpy(), drop.cpu().numpy())

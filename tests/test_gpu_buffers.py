@@ -322,9 +322,15 @@ def test_pool_keeps_only_the_newest_buffer():
     del bufs, t
     gc.collect()
     torch.cuda.synchronize()
+    # freeing never blocks (ABI 8): the two older buffers have retired but stay mapped until a call that may
+    # synchronise -- here the next allocation that maps new memory
+    assert rt.history_buffers_held(0)[1] == 3
+    w = E.history_buffer((1, 1 << 20, 8), torch.float32, DEV, chunk_bytes=64 << 20)
     nbytes, nbuf = rt.history_buffers_held(0)
     assert nbuf == 1 and nbytes == 4 << 32                       # the last one freed: 16 GiB
     assert torch.cuda.mem_get_info()[0] >= free0 - (16 << 30) - (512 << 20)
+    del w
+    gc.collect()
     rt.trim_history_buffers()
     assert torch.cuda.mem_get_info()[0] >= free0 - (512 << 20)
 
@@ -441,3 +447,51 @@ def test_writer_streams_large_histories_back_to_back(tmp_path):
         system.ray_trace(fan, m0, m1, dtype="float32", out=ref)
         assert np.array_equal(got[k].view(np.int32), ref.cpu().numpy().view(np.int32)), k
     C.check(C.lib().rtpb_buffer_trim())
+
+
+def test_trim_keeps_a_pool_whose_tensors_live():
+    """trim_history_buffers drops only history pools none of whose blocks is in use.  A live history
+    survives a trim with its pool (still counted by history_buffers_held once freed); freed, the next trim returns
+    its memory to the device."""
+    from ray_trace_pb_amd import _engine as E
+    rt.trim_history_buffers()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info()[0]
+    t = rt.history_buffer((4, 1 << 28, 8), torch.float32, DEV)            # 32 GiB in the history pool
+    t[-1, -1].fill_(3.0)
+    pid = E.history_pool(0).id
+    rt.trim_history_buffers()
+    assert E._POOL_IDS.get(0) == pid                                     # kept: a tensor lives in it
+    torch.cuda.synchronize()
+    assert float(t[-1, -1, -1]) == 3.0
+    del t
+    gc.collect()
+    assert rt.history_buffers_held(0)[0] >= 32 << 30                     # cached, and counted
+    rt.trim_history_buffers()
+    assert 0 not in E._POOL_IDS                                          # dropped now
+    assert rt.history_buffers_held(0) == (0, 0)
+    assert torch.cuda.mem_get_info()[0] >= free0 - (512 << 20)
+
+
+def test_trim_allocate_cycles_grow_dead_va_by_one_segment_each():
+    """every released history-pool segment keeps its virtual range reserved, so a
+    trim -> allocate cycle adds exactly that segment's size to the dead address space -- a bounded, linear cost:
+    at a C3-size history (30.4 GB) the default 32 TiB limit allows ~1,150 such cycles before new histories fall
+    back to plain hipMalloc (still correct, test_dead_va_limit_falls_back_to_plain_allocations)."""
+    from ray_trace_pb_amd import _engine as E
+    rt.trim_history_buffers()
+    seg = None
+    dead = [E.buffer_stats()["dead_va_bytes"]]
+    for k in range(4):
+        t = rt.history_buffer((1, 1 << 27, 8), torch.float32, DEV)        # 4 GiB
+        t[0, -1].fill_(float(k))
+        seg = E.buffer_stats()["pool_bytes"]
+        del t
+        gc.collect()
+        rt.trim_history_buffers()
+        dead.append(E.buffer_stats()["dead_va_bytes"])
+    steps = [b - a for a, b in zip(dead, dead[1:])]
+    assert all(d == steps[0] for d in steps) and steps[0] >= 4 << 30 and steps[0] <= seg
+    limit = E.buffer_stats()["dead_va_limit"]
+    assert limit // (19 * 50_007_030 * 8 * 4) >= 1000

@@ -59,3 +59,26 @@ def test_library_never_reserves_a_released_range_again():
         gc.collect()
         rt.trim_history_buffers()                                           # release: the range stays reserved
     assert E.buffer_stats()["dead_va_bytes"] >= dead0 + 6 * (192 << 20)
+
+
+def test_vmm_remap_check_on_torch_runtime():
+    """The same check on torch's HIP runtime (tools/vmm_torch_runtime.py: the shared-library build loaded after
+    torch, bound to the libamdhip64 torch ships): fresh ranges and kernel reads must be right; the verdict on
+    remapped ranges is reported, not asserted."""
+    import sys
+    tool = os.path.join(os.path.dirname(HERE), "tools", "vmm_torch_runtime.py")
+    r = subprocess.run([sys.executable, tool, "6"], capture_output=True, text=True, timeout=240)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "HIP runtimes mapped: [" in r.stdout and "torch/lib/libamdhip64" in r.stdout
+    cases = {}
+    for line in r.stdout.splitlines():
+        m = re.match(r"CASE (\S+)\s+fresh_maps=(\d+) bad\(kernel,copy\)=(\d+),(\d+)\s+reused_maps=(\d+) "
+                     r"bad\(kernel,copy\)=(\d+),(\d+)\s+live_remap bad\(kernel,copy\)=(\d+),(\d+)\s+victim_bad=(\d+)",
+                     line)
+        if m:
+            cases[m.group(1)] = [int(v) for v in m.groups()[1:]]
+    assert len(cases) == 6
+    for name, (nf, fk, fc, nr, rk, rc, lk, lc, vb) in cases.items():
+        assert fk == 0 and fc == 0, (name, "a fresh range read back wrong")
+        assert rk == 0 and vb == 0, (name, "kernel reads / victim memory changed")

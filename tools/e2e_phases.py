@@ -93,7 +93,7 @@ def main():
     torch.cuda.synchronize()
 
     # (3) the drop-in call as the bench times it, phase by phase
-    for name in ("lower", "tabulated", "table_fingerprint", "previous_keys", "trace_device", "history_buffer",
+    for name in ("memo_lookup", "memo_store", "lower", "tabulated", "table_fingerprint", "previous_keys", "trace_device", "history_buffer",
                  "distinct_wavelengths", "pool_empty", "device_empty", "history_pool", "resolve_planes"):
         wrap(E, name)
     wrap(R, "_default_history")

@@ -22,6 +22,10 @@
 #                    (tools/placement_channels.py under rocprofv3 --pmc, JSON output: one value per instance)
 #   counters         rocprofv3 -L (the PMC counters and their dimensions on this box)
 #   vmm              tests/native/vmm_remap_check (HIP virtual-memory remapping, no torch; built in-tree)
+#   vmmtorch         the same check on torch's HIP runtime (tools/vmm_torch_runtime.py)
+#   e2e:CONFIG       host phases of the drop-in call for one bench config (e2e:c2)
+#   dangling         round 5's MemPool crash reproduced in child processes (tools/mempool_dangling.py): a child
+#                    killed by SIGSEGV is the expected result of one case, so this must be the LAST step
 #   valu             issue cost of the kernels' VALU instructions (tools/valu/valu_rates.hip, built in-tree)
 #   ab:LIB[,LIB..]   A/B of the in-tree library against experiment builds (tools/ab_variants.py, histories;
 #                    C5 sweep per library, the in-tree one before and after)
@@ -63,6 +67,9 @@ for s in "$@"; do
     pmc_c4) step pmc_c4 900 bash tools/pmc_kernel.sh "$P/pmc_c4" trace_kernel python3 tools/run_variant.py --config c4:1.0 --reps 2 ;;
     pmc_c5) step pmc_c5 900 bash tools/pmc_kernel.sh "$P/pmc_c5" sweep_kernel python3 tools/c5_sweep.py --fields 1 --warmup 0 ;;
     e2e) step e2e 600 python3 tools/e2e_phases.py ;;
+    e2e:*) step "e2e_${s#e2e:}" 600 python3 tools/e2e_phases.py --config "${s#e2e:}" --reps 31 ;;
+    vmmtorch) step vmm_torch_runtime 300 python3 tools/vmm_torch_runtime.py 10 ;;
+    dangling) step mempool_dangling 300 python3 tools/mempool_dangling.py ;;
     valu) step valu 300 tools/valu/_build/valu_rates ;;
     vmm) step vmm 300 tests/native/_build/vmm_remap_check 10 ;;
     counters) step counters 120 rocprofv3 -L ;;
