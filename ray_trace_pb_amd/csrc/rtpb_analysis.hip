@@ -261,10 +261,10 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
     auto trace_from = [&](int s) {
         while (s < a.nsurf) {
             const int code = code_of(s);
-            dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto ax) {
+            dispatch_code<(FEAT & 1) != 0>(code, [&](auto kind, auto geo) {
                 constexpr int K = decltype(kind)::value;
-                constexpr bool A = decltype(ax)::value;
-                constexpr bool kCarry = K == SPHERE && A;
+                constexpr int A = decltype(geo)::value;
+                constexpr bool kCarry = K == SPHERE && A == kGeoAxial;
                 if constexpr (kCarry) {
 #pragma unroll
                     for (int q = 0; q < kSweepRays; ++q) rxy[q] = r[q].x * r[q].x + r[q].y * r[q].y;
@@ -344,32 +344,34 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
         wl0 = rg.wl;
         const int code0 = a.nsurf > 0 ? code_of(0) : -1;
         using std::integral_constant;
-        // fn(kind, ax) on the first surface's code when it is a refracting Flat / Sphere; false otherwise
+        // fn(kind, geo) on the first surface's code when it is a refracting Flat / Sphere; false otherwise
         auto on_first = [&](auto&& fn) {
-            if (code0 == 2 * SPHERE + 1) fn(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
-            else if (code0 == 2 * SPHERE) fn(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
-            else if (code0 == 2 * FLAT + 1) fn(integral_constant<int, FLAT>(), integral_constant<bool, true>());
-            else if (code0 == 2 * FLAT) fn(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+            if (code0 == 3 * SPHERE + kGeoAxial) fn(integral_constant<int, SPHERE>(), integral_constant<int, kGeoAxial>());
+            else if (code0 == 3 * SPHERE) fn(integral_constant<int, SPHERE>(), integral_constant<int, kGeoGeneral>());
+            else if (code0 == 3 * FLAT + kGeoAxial) fn(integral_constant<int, FLAT>(), integral_constant<int, kGeoAxial>());
+            else if (code0 == 3 * FLAT + kGeoXZ) fn(integral_constant<int, FLAT>(), integral_constant<int, kGeoXZ>());
+            else if (code0 == 3 * FLAT) fn(integral_constant<int, FLAT>(), integral_constant<int, kGeoGeneral>());
             else return false;
             return true;
         };
         // the shared part of the first surface (surface_step_pair): a row that fails the front-side or on-surface
         // test stores a NaN position and c . d, so each refraction of it is all NaN (as the step's kill)
-        const bool shared = on_first([&](auto kind, auto ax) {
+        const bool shared = on_first([&](auto kind, auto geo) {
             constexpr int K = decltype(kind)::value;
-            constexpr bool A = decltype(ax)::value;
+            constexpr int A = decltype(geo)::value;
             const DevSurface<double> base = load_surface<double>(surf);
             const Rcp<double> iwl0 = make_wl_rcp(rg.wl);     // (the phase, and with it n1 and iwl0, is not kept)
             double rxy0 = rg.x * rg.x + rg.y * rg.y;
             double Nx, Ny, Nz;
             Ray<double> ri;
+            bool fwd = true;
             hit_and_normal<double, K, A>(base, rg, 1.0, iwl0, static_cast<GuardBranch*>(nullptr),
-                                         K == SPHERE && A ? &rxy0 : nullptr, ri, Nx, Ny, Nz);
-            const bool front_ok = !front_side_fails<A, true>(rg, base);
-            constexpr bool kAxBasis = A && K == FLAT;
-            const SnellBasis<double> b = snell_basis<kAxBasis>(ri, Nx, Ny, Nz, static_cast<GuardBranch*>(nullptr));
+                                         K == SPHERE && A == kGeoAxial ? &rxy0 : nullptr, ri, Nx, Ny, Nz, &fwd);
+            const bool front_ok = !front_side_fails<A, true>(rg, base) && fwd;
+            constexpr int kBasis = K == FLAT ? A : kGeoGeneral;
+            const SnellBasis<double> b = snell_basis<kBasis>(ri, Nx, Ny, Nz, static_cast<GuardBranch*>(nullptr));
             bool ok;
-            if constexpr (K == SPHERE) ok = on_sphere<A>(ri, base, A ? &rxy0 : nullptr) && front_ok;
+            if constexpr (K == SPHERE) ok = on_sphere<A == kGeoAxial>(ri, base, A == kGeoAxial ? &rxy0 : nullptr) && front_ok;
             else ok = on_flat<A>(ri, base) && front_ok;
             double px = ri.x, py = ri.y, pz = ri.z, cd = b.cd;
             if (!ok) px = py = pz = cd = qnan<double>();
@@ -392,8 +394,8 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
                 r[q].wl = stored<TS>(a.grp[4 * grp[q] + 3]);
             }
             int s0 = 0;
-            const bool first = on_first([&](auto kind, auto ax) {
-                constexpr bool kAxBasis = decltype(ax)::value && decltype(kind)::value == FLAT;
+            const bool first = on_first([&](auto kind, auto geo) {
+                constexpr int kBasis = decltype(kind)::value == FLAT ? decltype(geo)::value : kGeoGeneral;
                 Ray<double> ri;
                 ri.x = state[0][tid]; ri.y = state[1][tid]; ri.z = state[2][tid];
                 ri.dx = ri.dy = ri.dz = 0.0;
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(kBlock) RTPB_SWEEP_ATTR void sweep_kernel(SweepArgs
 #pragma unroll
                 for (int q = 0; q < kSweepRays; ++q) {
                     ri.wl = r[q].wl;
-                    r[q] = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, gn[q][a.nsurf + 1],
+                    r[q] = snell_apply<kBasis, false>(ri, Nx, Ny, Nz, b, gn[q][a.nsurf + 1],
                                                         static_cast<GuardBranch*>(nullptr));
                 }
             });

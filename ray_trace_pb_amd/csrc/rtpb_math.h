@@ -248,7 +248,13 @@ RTPB_HD T np_sign(T v) {
 // bit for bit -- zero signs, infinities and NaN included (an fma rounds once, and a product that is exact
 // leaves nothing to round) -- and the reference's expressions shrink without changing a result:
 //   ((x - 0) * 0 + (y - 0) * 0) + (z - cz) * 1  ==  fma(y, 0, x * 0) + (z - cz)      (5 -> 3 float64 ops)
-// The specialised surface steps (surface_step<..., AX = true>) use only these identities.
+// The specialised surface steps (surface_step<..., GEO = kGeoAxial>) use only these identities.
+//
+// A surface TILTED in the x-z plane (the OPM's remote-focus optics, RT:1306-1347 / RT:1558-1801 with a normal
+// (-sin t, 0, cos t)) has normal, input axis and center with y components exactly +0: the same identities remove
+// every product with those zeros (kPlaneXZ, GEO = kGeoXZ) -- a dot product with the normal becomes
+// fma(vy, 0, vx nx) + vz nz (5 -> 4 float64 operations), a cross product with it loses two of its six products, and
+// y - (+0) = y.
 constexpr int32_t kAxial = 64;
 // rcp_ok bit 7: a PerfectLens with 2^-80 <= |focal_len| < 2^120, so -|r1| / f is inside the shortcut range
 constexpr int32_t kLensQ1 = 128;
@@ -262,24 +268,45 @@ constexpr int32_t kLensUniVac = 512;
 // quotients then need no div_fixup, fastdiv_q_nofix)
 constexpr int32_t kRPos = 1024;
 constexpr int32_t kRNeg = 2048;
+// rcp_ok bit 12: the x-z-plane geometry (flats and PerfectLens steps; set only where kAxial is not)
+constexpr int32_t kPlaneXZ = 4096;
+
+// geometry forms of the surface steps (template parameter GEO)
+constexpr int kGeoGeneral = 0;     // any normal, input axis and center
+constexpr int kGeoAxial = 1;       // kAxial: normal and input axis (+0, +0, 1), center (+0, +0, cz)
+constexpr int kGeoXZ = 2;          // kPlaneXZ: normal, input axis and center with y == +0
 
 RTPB_HD double tfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-// v . n for a surface vector n; AX: n == (+0, +0, 1)
-template <bool AX, typename T>
+// v . n for a surface vector n; kGeoAxial: n == (+0, +0, 1); kGeoXZ: ny == +0
+template <int GEO, typename T>
 RTPB_HD T axdot(T vx, T vy, T vz, T nx, T ny, T nz) {
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         (void)nx; (void)ny; (void)nz;
         return tfma(vy, T(0), vx * T(0)) + vz;
+    } else if constexpr (GEO == kGeoXZ) {
+        (void)ny;
+        return tfma(vy, T(0), vx * nx) + vz * nz;
     } else {
         return vx * nx + vy * ny + vz * nz;
     }
 }
 
-// v - c for the x / y component of a surface center; AX: c == +0
-template <bool AX, typename T>
-RTPB_HD T axsub(T v, T c) {
-    if constexpr (AX) {
+// v - c for the x component of a surface center; kGeoAxial: c == +0
+template <int GEO, typename T>
+RTPB_HD T axsub_x(T v, T c) {
+    if constexpr (GEO == kGeoAxial) {
+        (void)c;
+        return v;
+    } else {
+        return v - c;
+    }
+}
+
+// v - c for the y component of a surface center; kGeoAxial, kGeoXZ: c == +0
+template <int GEO, typename T>
+RTPB_HD T axsub_y(T v, T c) {
+    if constexpr (GEO != kGeoGeneral) {
         (void)c;
         return v;
     } else {
@@ -593,12 +620,12 @@ RTPB_HD bool table_has_key(const DevMaterial<T>& m, T wl, TablePtr table) {
 // ------------------------------------------------------------------ propagate_ray2plane (RT:241-306)
 // Returns the ray moved onto the plane {(p - c).nrm = 0}; phase += |d t| sign(t) 2pi/wl n.
 // iden: optional make_rcp of the denominator d.nrm, shared by several planes with the same normal.
-// AXN: the normal is (+0, +0, 1); AXC: cx and cy are +0 (axdot / axsub).
-template <bool AXN = false, bool AXC = false, typename T, class G = GuardBranch>
+// GN: the normal's geometry form, GC: the center's (axdot / axsub_x / axsub_y).
+template <int GN = kGeoGeneral, int GC = kGeoGeneral, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n, bool exclude_backward,
                         const Rcp<T>& iwl, T* t_out = nullptr, const Rcp<T>* iden = nullptr, G* g = nullptr) {
-    const T num = -axdot<AXN>(axsub<AXC>(r.x, cx), axsub<AXC>(r.y, cy), r.z - cz, nx, ny, nz);
-    const T den = axdot<AXN>(r.dx, r.dy, r.dz, nx, ny, nz);
+    const T num = -axdot<GN>(axsub_x<GC>(r.x, cx), axsub_y<GC>(r.y, cy), r.z - cz, nx, ny, nz);
+    const T den = axdot<GN>(r.dx, r.dy, r.dz, nx, ny, nz);
     const T t = iden ? div1_as(num, den, *iden, g) : num / den;
     const T s = t < T(0) ? T(-1) : T(1);
     const T vx = r.dx * t, vy = r.dy * t, vz = r.dz * t;
@@ -626,11 +653,21 @@ RTPB_HD Ray<T> to_plane(const Ray<T>& r, T nx, T ny, T nz, T cx, T cy, T cz, T n
 // (tests/test_gpu_fastdiv.py checks it against the reference's chain on adversarial B, root).
 // One product: with u2 = -B - root, 0.5 u2 >= 0 exactly when u2 >= -2^-1074 (half the smallest denormal rounds to
 // -0, to even; NaN fails both), so the halving can follow the choice.
-template <typename T>
-RTPB_HD T sphere_root(T B, T root) {
+//
+// FWD (the positions-only steps of kAxial spheres, whose finite shell_hi bounds every on-sphere point): no NaN for a
+// root outside [0, inf) -- *fwd reports whether the chosen root is forward, u1 >= -2^-1074 (u1 >= u2: a forward u2 is
+// chosen whenever there is one; NaN fails), and the caller folds it into the row's final kill.  A backward root gives
+// a point ON the sphere (killed through *fwd), an infinite one a point off every finite shell (killed by the
+// on-surface test) -- the row ends all NaN as with the reference's NaN t, and no stored value reads the position.
+template <bool FWD = false, typename T>
+RTPB_HD T sphere_root(T B, T root, bool* fwd = nullptr) {
     const T u1 = -B + root;
     const T u2 = -B - root;
     T t = T(0.5) * (u2 >= -std::numeric_limits<T>::denorm_min() ? u2 : u1);
+    if constexpr (FWD) {
+        *fwd = u1 >= -std::numeric_limits<T>::denorm_min();
+        return t;
+    }
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (sizeof(T) == 8) {
         // the NaN's high word from a scalar register (a VOP2 select's first operand), not a VGPR constant
@@ -642,15 +679,35 @@ RTPB_HD T sphere_root(T B, T root) {
     return t;
 }
 
+// sqrt(B^2 - 4C) of the sphere's quadratic (RT:1503).  FWD (positions-only axial steps, see sphere_root): the
+// argument is never -0 (B B >= +0), and of the arguments the square-root core cannot take only +0 and
+// 0 < v < 2^-767 need the full sequence -- for +inf the core's NaN instead of +inf kills the row exactly as the
+// reference's t = inf -> NaN does (sphere_root<true> reports no forward root) -- so ONE unsigned compare of the bit
+// pattern guards the core (negative and NaN arguments give NaN either way).
+template <bool FWD, typename T, class G>
+RTPB_HD T disc_root(T v, G* g) {
+#if defined(RTPB_FASTSQRT)
+    if constexpr (FWD && sizeof(T) == 8 && !G::kDefer) {
+        T root = sqrt_core(v);
+        if (__builtin_expect(__builtin_bit_cast(uint64_t, v) < 0x1000000000000000ull, 0)) root = sqrt(v);  // v < 2^-767
+        return root;
+    }
+#endif
+    return tsqrt<T>(v, g);
+}
+
 // rxy (AX only): x x + y y of the ray's position, as on_sphere computed it at the previous axial surface (the
-// same expression for a center on the axis) -- or nullptr
+// same expression for a center on the axis) -- or nullptr.  fwd: FWD roots (sphere_root<true>), else nullptr.
 template <bool AX = false, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> sphere_hit(const Ray<T>& r, const DevSurface<T>& s, T n, const Rcp<T>& iwl, G* g = nullptr,
-                          const T* rxy = nullptr) {
-    const T ox = axsub<AX>(r.x, s.c[0]), oy = axsub<AX>(r.y, s.c[1]), oz = r.z - s.c[2];
+                          const T* rxy = nullptr, bool* fwd = nullptr) {
+    constexpr int GEO = AX ? kGeoAxial : kGeoGeneral;
+    const T ox = axsub_x<GEO>(r.x, s.c[0]), oy = axsub_y<GEO>(r.y, s.c[1]), oz = r.z - s.c[2];
     const T B = T(2) * (r.dx * ox + r.dy * oy + r.dz * oz);
     const T C = ((AX && rxy) ? *rxy : ox * ox + oy * oy) + oz * oz - s.R2;
-    const T t = sphere_root(B, tsqrt<T>(B * B - T(4) * C, g));
+    T t;
+    if (AX && fwd) t = sphere_root<true>(B, disc_root<true>(B * B - T(4) * C, g), fwd);
+    else t = sphere_root(B, tsqrt<T>(B * B - T(4) * C, g));
     Ray<T> o;
     o.x = r.x + r.dx * t;
     o.y = r.y + r.dy * t;
@@ -741,7 +798,7 @@ RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
             // the reciprocal's offset, m >= 0 ? -2m : ceil(-m / 2) with m = d >> 1, in terms of d and as a bit select:
             // d >= 0 ? -(d & ~1) : (3 - d) >> 2
             const int32_t t = bit_select(neg, (3 - d) >> 2, -(d & ~1));
-            const double s = __hiloint2double(0x3FF00000 + neg, d >> 1);
+            const double s = __hiloint2double(__double2hiint(v), d >> 1);   // hi(v) = 0x3FF00000 + neg here
             const double yr = __hiloint2double(0x3FF00000 + (t >> 31), t);
             div3_norm<T, G, 1>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // components at most ~1: no fixup
             return;
@@ -752,24 +809,33 @@ RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
 }
 
 // basis (normal, nb, nc): nb = d x N / |.|, nc = N x nb / |.|  (RT:1203-1209 / RT:1271-1277)
-// AX: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot)
-template <bool AX = false, typename T, class G = GuardBranch>
+// kGeoAxial: N == (+0, +0, 1), so each cross-product component has at most one inexact product (axdot);
+// kGeoXZ: Ny == +0, the x and z components lose a product each: RN(p - RN(a 0)) == fma(-a, 0, p)
+template <int GEO = kGeoGeneral, typename T, class G = GuardBranch>
 RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
     T bx, by, bz;
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         bx = tfma(-ri.dz, T(0), ri.dy);                   // dy * 1 - dz * 0
         by = tfma(ri.dz, T(0), -ri.dx);                   // dz * 0 - dx * 1
         bz = tfma(-ri.dy, T(0), ri.dx * T(0));            // dx * 0 - dy * 0
+    } else if constexpr (GEO == kGeoXZ) {
+        bx = tfma(-ri.dz, T(0), ri.dy * Nz);              // dy Nz - dz * 0
+        by = ri.dz * Nx - ri.dx * Nz;
+        bz = tfma(ri.dx, T(0), -(ri.dy * Nx));            // dx * 0 - dy Nx
     } else {
         bx = ri.dy * Nz - ri.dz * Ny;
         by = ri.dz * Nx - ri.dx * Nz;
         bz = ri.dx * Ny - ri.dy * Nx;
     }
     unit_or_zero(bx, by, bz, g);
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
         cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
         cz = tfma(-bx, T(0), by * T(0));                  // 0 * by - 0 * bx
+    } else if constexpr (GEO == kGeoXZ) {
+        cx = tfma(bz, T(0), -(Nz * by));                  // 0 * bz - Nz by
+        cy = Nz * bx - Nx * bz;
+        cz = tfma(-bx, T(0), Nx * by);                    // Nx by - 0 * bx
     } else {
         cx = Ny * bz - Nz * by;
         cy = Nz * bx - Nx * bz;
@@ -800,25 +866,29 @@ struct SnellBasis {
     T cx, cy, cz, cd, nd;
 };
 
-template <bool AX = false, typename T, class G = GuardBranch>
+template <int GEO = kGeoGeneral, typename T, class G = GuardBranch>
 RTPB_HD SnellBasis<T> snell_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
     SnellBasis<T> b;
-    tangent_basis<AX>(ri, Nx, Ny, Nz, b.cx, b.cy, b.cz, g);
+    tangent_basis<GEO>(ri, Nx, Ny, Nz, b.cx, b.cy, b.cz, g);
     b.cd = b.cx * ri.dx + b.cy * ri.dy + b.cz * ri.dz;
-    b.nd = axdot<AX>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz);
+    b.nd = axdot<GEO>(ri.dx, ri.dy, ri.dz, Nx, Ny, Nz);
     return b;
 }
 
 // The refracted ray from the basis and the Snell ratio n1 / n2
-template <bool AX = false, bool TIR_FILL = true, typename T, class G = GuardBranch>
+template <int GEO = kGeoGeneral, bool TIR_FILL = true, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell_apply(const Ray<T>& ri, T Nx, T Ny, T Nz, const SnellBasis<T>& b, T ratio, G* g = nullptr) {
     const T mag = ratio * b.cd;
     const T tang = signed_root(b.nd, tsqrt_1m<T>(T(1) - mag * mag, g));
     Ray<T> o;
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         o.dx = tfma(tang, T(0), mag * b.cx);
         o.dy = tfma(tang, T(0), mag * b.cy);
         o.dz = mag * b.cz + tang;
+    } else if constexpr (GEO == kGeoXZ) {
+        o.dx = mag * b.cx + tang * Nx;
+        o.dy = tfma(tang, T(0), mag * b.cy);              // mag cy + tang * 0
+        o.dz = mag * b.cz + tang * Nz;
     } else {
         o.dx = mag * b.cx + tang * Nx;
         o.dy = mag * b.cy + tang * Ny;
@@ -835,9 +905,9 @@ RTPB_HD Ray<T> snell_apply(const Ray<T>& ri, T Nx, T Ny, T Nz, const SnellBasis<
     return o;
 }
 
-template <bool AX = false, bool TIR_FILL = true, typename T, class G = GuardBranch>
+template <int GEO = kGeoGeneral, bool TIR_FILL = true, typename T, class G = GuardBranch>
 RTPB_HD Ray<T> snell(const Ray<T>& ri, T Nx, T Ny, T Nz, T ratio, G* g = nullptr) {
-    return snell_apply<AX, TIR_FILL>(ri, Nx, Ny, Nz, snell_basis<AX>(ri, Nx, Ny, Nz, g), ratio, g);
+    return snell_apply<GEO, TIR_FILL>(ri, Nx, Ny, Nz, snell_basis<GEO>(ri, Nx, Ny, Nz, g), ratio, g);
 }
 
 // law of reflection (RT:1267-1289)
@@ -861,10 +931,10 @@ RTPB_HD Ray<T> reflect(const Ray<T>& ri, T Nx, T Ny, T Nz, G* g = nullptr) {
 }
 
 // FlatSurface / PlaneMirror .is_pt_on_surface (RT:1339-1347, RT:1405-1412)
-template <bool AX = false, typename T>
+template <int GEO = kGeoGeneral, typename T>
 RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
-    const T rx = axsub<AX>(p.x, s.c[0]), ry = axsub<AX>(p.y, s.c[1]), rz = p.z - s.c[2];
-    const T h = axdot<AX>(rx, ry, rz, s.nrm[0], s.nrm[1], s.nrm[2]);
+    const T rx = axsub_x<GEO>(p.x, s.c[0]), ry = axsub_y<GEO>(p.y, s.c[1]), rz = p.z - s.c[2];
+    const T h = axdot<GEO>(rx, ry, rz, s.nrm[0], s.nrm[1], s.nrm[2]);
     return tabs<T>(h) < s.tol && rx * rx + ry * ry + rz * rz <= s.ap_sq;      // norm(p - c) <= aperture
 }
 
@@ -874,7 +944,8 @@ RTPB_HD bool on_flat(const Ray<T>& p, const DevSurface<T>& s) {
 // (qx qx + qy qy) + qz qz is exactly p.x p.x + p.y p.y -- the first partial sum of d2.
 template <bool AX = false, typename T>
 RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s, T* rxy_out = nullptr) {
-    const T rx = axsub<AX>(p.x, s.c[0]), ry = axsub<AX>(p.y, s.c[1]), rz = p.z - s.c[2];
+    constexpr int GEO = AX ? kGeoAxial : kGeoGeneral;
+    const T rx = axsub_x<GEO>(p.x, s.c[0]), ry = axsub_y<GEO>(p.y, s.c[1]), rz = p.z - s.c[2];
     const T rxy = rx * rx + ry * ry;
     if (rxy_out) *rxy_out = rxy;
     const T d2 = rxy + rz * rz;
@@ -892,15 +963,15 @@ RTPB_HD bool on_sphere(const Ray<T>& p, const DevSurface<T>& s, T* rxy_out = nul
 // The "at" plane (the lens plane, RT:1790-1793) is emitted first: it depends on r only.
 // UNI: the media on both sides are uniform (Constant, or Vacuum with an ordinary wavelength on every lane of the
 // wave): F, B, n1 f and n1 n1 f + n2 n2 f come from the descriptor, computed on the host by the same operations.
-template <typename T, bool AX, bool UNI, typename EmitAt, class G>
+template <typename T, int GEO, bool UNI, typename EmitAt, class G>
 RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                        Ray<T>& after, G* g) {
     const T f = s.f;
     const T nx = s.nrm[0], ny = s.nrm[1], nz = s.nrm[2];
     // the "before" plane and the front focal plane share the normal, so d.n divides both (one Rcp)
-    const Rcp<T> iden = make_rcp(axdot<AX>(r.dx, r.dy, r.dz, nx, ny, nz));
-    emit_at(to_plane<AX, AX>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
-                             g));   // RT:1790-1793
+    const Rcp<T> iden = make_rcp(axdot<GEO>(r.dx, r.dy, r.dz, nx, ny, nz));
+    emit_at(to_plane<GEO, GEO>(r, nx, ny, nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, static_cast<T*>(nullptr), &iden,
+                               g));   // RT:1790-1793
     T Fx, Fy, Fz, Bx, By, Bz;
     if constexpr (UNI) {
         Fx = s.lF[0]; Fy = s.lF[1]; Fz = s.lF[2];
@@ -909,22 +980,27 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
         Fx = s.c[0] - s.nf[0] * n1; Fy = s.c[1] - s.nf[1] * n1; Fz = s.c[2] - s.nf[2] * n1;
         Bx = s.c[0] + s.nf[0] * n2; By = s.c[1] + s.nf[1] * n2; Bz = s.c[2] + s.nf[2] * n2;
     }
-    // axial and uniform: F = (+0, +0, Fz), so the front focal plane has the axial center form too
-    constexpr bool AXF = AX && UNI;
-    const Ray<T> rf = to_plane<AX, AXF>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
-    const T dn = axdot<AX>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
+    // axial (x-z plane) and uniform: the host checked F = (+0, +0, Fz) (Fy = +0), so the front focal plane has the
+    // surface's center form too
+    constexpr int GF = UNI ? GEO : kGeoGeneral;
+    const Ray<T> rf = to_plane<GEO, GF>(r, nx, ny, nz, Fx, Fy, Fz, n1, false, iwl, static_cast<T*>(nullptr), &iden, g);
+    const T dn = axdot<GEO>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
     T spx, spy, spz;
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         spx = tfma(-dn, T(0), rf.dx);                 // dx - dn * 0
         spy = tfma(-dn, T(0), rf.dy);
         spz = rf.dz - dn;                             // dz - dn * 1
+    } else if constexpr (GEO == kGeoXZ) {
+        spx = rf.dx - dn * nx;
+        spy = tfma(-dn, T(0), rf.dy);                 // dy - dn * 0
+        spz = rf.dz - dn * nz;
     } else {
         spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
     }
     // |s1_perp| and |r1| (RT:1704-1728): a norm squared in range takes the combined test (norm2_fast), the
     // rest the full tests -- bit-identical either way, NaN included
     const T spv = spx * spx + spy * spy + spz * spz;
-    const T r1x = axsub<AXF>(rf.x, Fx), r1y = axsub<AXF>(rf.y, Fy), r1z = rf.z - Fz;
+    const T r1x = axsub_x<GF>(rf.x, Fx), r1y = axsub_y<GF>(rf.y, Fy), r1z = rf.z - Fz;
     const T r1v = r1x * r1x + r1y * r1y + r1z * r1z;
     T ux = r1x, uy = r1y, uz = r1z;
     T r1n;
@@ -974,10 +1050,14 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
         sin_t2 = q1 / n2;
     }
     const T cos_t2 = tsqrt_1m<T>(T(1) - sin_t2 * sin_t2, g);
-    if constexpr (AX) {
+    if constexpr (GEO == kGeoAxial) {
         o.dx = tfma(cos_t2, T(0), sin_t2 * ux);
         o.dy = tfma(cos_t2, T(0), sin_t2 * uy);
         o.dz = sin_t2 * uz + cos_t2;
+    } else if constexpr (GEO == kGeoXZ) {
+        o.dx = sin_t2 * ux + cos_t2 * nx;
+        o.dy = tfma(cos_t2, T(0), sin_t2 * uy);       // sin_t2 uy + cos_t2 * 0
+        o.dz = sin_t2 * uz + cos_t2 * nz;
     } else {
         o.dx = sin_t2 * ux + cos_t2 * nx;
         o.dy = sin_t2 * uy + cos_t2 * ny;
@@ -989,8 +1069,8 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     // 2 pi / wl (RT:1773): the ray's wavelength is wl0 or NaN, and where it is NaN rf.ph is NaN already
     const T k = iwl.k;
     o.ph = rf.ph - k * n1 * pw + k * (UNI ? s.lph : n1 * n1 * f + n2 * n2 * f);
-    after = to_plane<AX, AX>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
-                             static_cast<const Rcp<T>*>(nullptr), g);
+    after = to_plane<GEO, GEO>(o, nx, ny, nz, s.c[0], s.c[1], s.c[2], n2, false, iwl, static_cast<T*>(nullptr),
+                               static_cast<const Rcp<T>*>(nullptr), g);
 }
 
 // The front-side test d . input_axis < 0 (RT:1187-1192).  POS_ONLY (the sweep's final-position semantics) on an
@@ -999,25 +1079,29 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
 // intersection and are killed by the on-surface test either way (only their unstored at-plane differs): dz < 0
 // alone.  (A class-test form of the exact test -- dz < 0 with dx, dy finite -- measured no cheaper in the history
 // kernels: the compiler then keeps register copies for the kill.)
-template <bool AX, bool POS_ONLY, typename T>
+template <int GEO, bool POS_ONLY, typename T>
 RTPB_HD bool front_side_fails(const Ray<T>& r, const DevSurface<T>& s) {
-    if constexpr (AX && POS_ONLY) {
+    if constexpr (GEO == kGeoAxial && POS_ONLY) {
         (void)s;
         return r.dz < T(0);
     } else {
-        return axdot<AX>(r.dx, r.dy, r.dz, s.ax[0], s.ax[1], s.ax[2]) < T(0);
+        return axdot<GEO>(r.dx, r.dy, r.dz, s.ax[0], s.ax[1], s.ax[2]) < T(0);
     }
 }
 
 // The intersection and the surface normal there (RefractingSurface / ReflectingSurface.propagate RT:1181-1186 with
 // get_intersect / get_normal of FlatSurface RT:1323-1337, PlaneMirror RT:1398-1403, SphericalSurface RT:1467-1516)
-template <typename T, int KIND, bool AX, class G>
+// fwd (positions-only steps): the kAxial sphere's forward-root flag (sphere_root<true>) for the row's final kill; left
+// as it is for other surfaces
+template <typename T, int KIND, int GEO, class G>
 RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const Rcp<T>& iwl, G* g, T* rxy, Ray<T>& ri,
-                            T& Nx, T& Ny, T& Nz) {
+                            T& Nx, T& Ny, T& Nz, bool* fwd = nullptr) {
     if constexpr (KIND == SPHERE) {
-        ri = sphere_hit<AX>(r, s, n1, iwl, g, static_cast<const T*>(rxy));
-        Nx = axsub<AX>(ri.x, s.c[0]);                                  // (p - c) / R, RT:1476
-        Ny = axsub<AX>(ri.y, s.c[1]);
+        static_assert(GEO != kGeoXZ, "x-z plane steps: flats and PerfectLens only");
+        constexpr bool AX = GEO == kGeoAxial;
+        ri = sphere_hit<AX>(r, s, n1, iwl, g, static_cast<const T*>(rxy), AX ? fwd : nullptr);
+        Nx = axsub_x<GEO>(ri.x, s.c[0]);                               // (p - c) / R, RT:1476
+        Ny = axsub_y<GEO>(ri.y, s.c[1]);
         Nz = ri.z - s.c[2];
         if constexpr (AX) {
             // kAxial spheres have a finite shell_hi: where the on-surface test passes (the only rays whose
@@ -1040,8 +1124,8 @@ RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const
         }
     } else {                                                           // FLAT, PLANE_MIRROR
         Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-        ri = to_plane<AX, AX>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
-                              static_cast<const Rcp<T>*>(nullptr), g);          // RT:1331-1337, 1398-1403
+        ri = to_plane<GEO, GEO>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
+                                static_cast<const Rcp<T>*>(nullptr), g);        // RT:1331-1337, 1398-1403
     }
 }
 
@@ -1050,7 +1134,7 @@ RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const
 // One surface of a known kind (KIND = PERFECT_LENS, SPHERE, FLAT or PLANE_MIRROR).  The "at" plane is
 // handed to emit_at as soon as it is final, so the kernel can stage it to LDS before the rest of the
 // surface is computed (the PerfectLens path computes it first: it depends on r only).
-// AX: the surface has kAxial geometry (not for PLANE_MIRROR).
+// GEO: kGeoAxial for kAxial geometry (not for PLANE_MIRROR), kGeoXZ for kPlaneXZ (FLAT, PERFECT_LENS only).
 // MODE kPosOnly: the spot sweep's final-position semantics (snell's TIR fill left to the next surface, see snell; the
 // front-side test folded into the final kill; no "at" plane: emit_at is not called).
 // rxy (kAxial spheres in kPosOnly runs): in: x x + y y of r (on_sphere's value at the previous axial surface); out:
@@ -1060,23 +1144,25 @@ constexpr int kPosOnly = 1;
 // e.g. the spot sweep, whose host evaluates every medium at the group's one wavelength): no per-lane division path,
 // and the ratio stays a scalar operand
 constexpr int kUniMedia = 2;
-template <typename T, int KIND, bool AX = false, int MODE = 0, typename EmitAt, class G = GuardBranch>
+template <typename T, int KIND, int GEO = kGeoGeneral, int MODE = 0, typename EmitAt, class G = GuardBranch>
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                           Ray<T>& after, G* g = nullptr, T* rxy = nullptr) {
     constexpr bool kTirFill = (MODE & kPosOnly) == 0;
+    constexpr bool AX = GEO == kGeoAxial;
     if constexpr (KIND == PERFECT_LENS) {
         // uniform media: the instantiation with the focal points and constants in scalar registers (a wave-uniform
         // branch between two whole steps: merged values would cost vector registers on both paths)
         if (s.rcp_ok & kLensUni) {
             RTPB_NO_SPECULATE();
-            lens_step<T, AX, true>(s, r, n1, n2, iwl, emit_at, after, g);
+            lens_step<T, GEO, true>(s, r, n1, n2, iwl, emit_at, after, g);
         } else {
-            lens_step<T, AX, false>(s, r, n1, n2, iwl, emit_at, after, g);
+            lens_step<T, GEO, false>(s, r, n1, n2, iwl, emit_at, after, g);
         }
     } else {
         T Nx, Ny, Nz;
         Ray<T> ri;
-        hit_and_normal<T, KIND, AX>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz);
+        bool fwd = true;
+        hit_and_normal<T, KIND, GEO>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz, (MODE & kPosOnly) != 0 ? &fwd : nullptr);
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
             after = reflect(ri, Nx, Ny, Nz, g);
@@ -1088,9 +1174,9 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
                 // positions only: the failure joins the on-surface kill of `after` below instead of filling ri with
                 // NaN first (6 register fills issued on every path) -- `after` is all NaN either way, and so is every
                 // later position of the row (its next intersection reads a NaN direction); emit_at is not called
-                ok = !front_side_fails<AX, true>(r, s);
+                ok = !front_side_fails<GEO, true>(r, s) && fwd;
             } else {
-                kill_if(front_side_fails<AX, false>(r, s), ri);
+                kill_if(front_side_fails<GEO, false>(r, s), ri);
                 emit_at(ri);
                 ok = true;
             }
@@ -1103,9 +1189,10 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
             } else {
                 ratio = n1 / n2;
             }
-            after = snell<AX && KIND == FLAT, kTirFill>(ri, Nx, Ny, Nz, ratio, g);
+            // the Snell normal of a flat is its own normal (its geometry form); a sphere's is per ray (general)
+            after = snell<KIND == FLAT ? GEO : kGeoGeneral, kTirFill>(ri, Nx, Ny, Nz, ratio, g);
             if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy) && ok;    // (rxy is written either way)
-            else ok = on_flat<AX>(ri, s) && ok;
+            else ok = on_flat<GEO>(ri, s) && ok;
             kill_if(!ok, after);
         }
     }
@@ -1116,84 +1203,102 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
 // for all of them -- the intersection, the normal, the front-side and on-surface tests and the tangent basis
 // (snell_basis) are computed once, the refraction (snell_apply) per ratio.  kPosOnly semantics only: the phase of
 // `after_b` is r's (the sweep reads positions); wl_b is the second ray's wavelength.
-template <typename T, int KIND, bool AX, int MODE, class G = GuardBranch>
+template <typename T, int KIND, int GEO, int MODE, class G = GuardBranch>
 RTPB_HD void surface_step_pair(const DevSurface<T>& s, const Ray<T>& r, T n1, const Rcp<T>& iwl, T ratio_a, T ratio_b,
                                T wl_b, Ray<T>& after_a, Ray<T>& after_b, G* g = nullptr, T* rxy = nullptr) {
     static_assert((MODE & kPosOnly) != 0 && (KIND == SPHERE || KIND == FLAT), "refracting surfaces, positions only");
     T Nx, Ny, Nz;
     Ray<T> ri;
-    hit_and_normal<T, KIND, AX>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz);
-    const bool front_ok = !front_side_fails<AX, true>(r, s);     // joins the final kill, as in surface_step
-    constexpr bool kAxBasis = AX && KIND == FLAT;
-    const SnellBasis<T> b = snell_basis<kAxBasis>(ri, Nx, Ny, Nz, g);
-    after_a = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, ratio_a, g);
-    after_b = snell_apply<kAxBasis, false>(ri, Nx, Ny, Nz, b, ratio_b, g);
+    bool fwd = true;
+    hit_and_normal<T, KIND, GEO>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz, &fwd);
+    const bool front_ok = !front_side_fails<GEO, true>(r, s) && fwd;     // joins the final kill, as in surface_step
+    constexpr int kBasis = KIND == FLAT ? GEO : kGeoGeneral;
+    const SnellBasis<T> b = snell_basis<kBasis>(ri, Nx, Ny, Nz, g);
+    after_a = snell_apply<kBasis, false>(ri, Nx, Ny, Nz, b, ratio_a, g);
+    after_b = snell_apply<kBasis, false>(ri, Nx, Ny, Nz, b, ratio_b, g);
     after_b.wl = wl_b;
     bool ok;
-    if constexpr (KIND == SPHERE) ok = on_sphere<AX>(ri, s, rxy) && front_ok;
-    else ok = on_flat<AX>(ri, s) && front_ok;
+    if constexpr (KIND == SPHERE) ok = on_sphere<GEO == kGeoAxial>(ri, s, rxy) && front_ok;
+    else ok = on_flat<GEO>(ri, s) && front_ok;
     kill_if(!ok, after_a);
     kill_if(!ok, after_b);
 }
 
-// Any surface: a wave-uniform switch on the kind (and on kAxial geometry): calls
-// step(integral_constant<int, KIND>, integral_constant<bool, AX>).  WITH_LENS = false compiles the
+// The geometry form of a surface's steps from its flags (kAxial, kPlaneXZ; a mirror and any sphere not kAxial run
+// the general form)
+RTPB_HD int surface_geo(int kind, int32_t rcp_ok) {
+    if (kind == PLANE_MIRROR) return kGeoGeneral;
+    if (rcp_ok & kAxial) return kGeoAxial;
+    return (kind != SPHERE && (rcp_ok & kPlaneXZ)) ? kGeoXZ : kGeoGeneral;
+}
+
+// Any surface: a wave-uniform switch on the kind and the geometry form: calls
+// step(integral_constant<int, KIND>, integral_constant<int, GEO>).  WITH_LENS = false compiles the
 // PerfectLens case out (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans
 // without PerfectLens surfaces (rtpb_plan::feat).
 template <bool WITH_LENS, typename T, typename Step>
 RTPB_HD void dispatch_kind(const DevSurface<T>& s, Step&& step) {
     using std::integral_constant;
     const int kind = s.kind;
-    const bool ax = (s.rcp_ok & kAxial) != 0;
+    const int geo = surface_geo(kind, s.rcp_ok);
     if (WITH_LENS && kind == PERFECT_LENS) {
         if constexpr (WITH_LENS) {
-            if (ax) step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, true>());
-            else step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, false>());
+            if (geo == kGeoAxial) step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoAxial>());
+            else if (geo == kGeoXZ) step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoXZ>());
+            else step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoGeneral>());
         }
     } else if (kind == SPHERE) {
-        if (ax) step(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
-        else step(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+        if (geo == kGeoAxial) step(integral_constant<int, SPHERE>(), integral_constant<int, kGeoAxial>());
+        else step(integral_constant<int, SPHERE>(), integral_constant<int, kGeoGeneral>());
     } else if (kind == PLANE_MIRROR) {
-        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<bool, false>());
-    } else if (ax) {
-        step(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<int, kGeoGeneral>());
+    } else if (geo == kGeoAxial) {
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoAxial>());
+    } else if (geo == kGeoXZ) {
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoXZ>());
     } else {
-        step(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoGeneral>());
     }
 }
 
-// The (kind, kAxial) pair of dispatch_kind as one integer, and the dispatch on it: a loop can run a whole RUN
+// The (kind, geometry form) pair of dispatch_kind as one integer, and the dispatch on it: a loop can run a whole RUN
 // of consecutive surfaces of one code inside one instantiation of the step (no per-surface join of the kind
 // branches, so the ray's registers carry over from surface to surface without copies)
 template <typename T>
 RTPB_HD int surface_code(int kind, int32_t rcp_ok) {
-    return 2 * kind + ((rcp_ok & kAxial) != 0 && kind != PLANE_MIRROR ? 1 : 0);
+    return 3 * kind + surface_geo(kind, rcp_ok);
 }
 
 template <bool WITH_LENS, typename Step>
 RTPB_HD void dispatch_code(int code, Step&& step) {
     using std::integral_constant;
     switch (code) {
-    case 2 * PERFECT_LENS + 1:
-        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, true>()); break; }
+    case 3 * PERFECT_LENS + kGeoAxial:
+        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoAxial>()); break; }
         [[fallthrough]];
-    case 2 * FLAT + 1:
-        step(integral_constant<int, FLAT>(), integral_constant<bool, true>());
+    case 3 * FLAT + kGeoAxial:
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoAxial>());
         break;
-    case 2 * SPHERE + 1:
-        step(integral_constant<int, SPHERE>(), integral_constant<bool, true>());
+    case 3 * PERFECT_LENS + kGeoXZ:
+        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoXZ>()); break; }
+        [[fallthrough]];
+    case 3 * FLAT + kGeoXZ:
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoXZ>());
         break;
-    case 2 * SPHERE:
-        step(integral_constant<int, SPHERE>(), integral_constant<bool, false>());
+    case 3 * SPHERE + kGeoAxial:
+        step(integral_constant<int, SPHERE>(), integral_constant<int, kGeoAxial>());
         break;
-    case 2 * PLANE_MIRROR:
-        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<bool, false>());
+    case 3 * SPHERE:
+        step(integral_constant<int, SPHERE>(), integral_constant<int, kGeoGeneral>());
         break;
-    case 2 * PERFECT_LENS:
-        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<bool, false>()); break; }
+    case 3 * PLANE_MIRROR:
+        step(integral_constant<int, PLANE_MIRROR>(), integral_constant<int, kGeoGeneral>());
+        break;
+    case 3 * PERFECT_LENS:
+        if constexpr (WITH_LENS) { step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoGeneral>()); break; }
         [[fallthrough]];
     default:
-        step(integral_constant<int, FLAT>(), integral_constant<bool, false>());
+        step(integral_constant<int, FLAT>(), integral_constant<int, kGeoGeneral>());
         break;
     }
 }
@@ -1201,8 +1306,8 @@ RTPB_HD void dispatch_code(int code, Step&& step) {
 template <typename T, bool WITH_LENS = true, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
                                     EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
-    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto ax) {
-        surface_step<T, decltype(kind)::value, decltype(ax)::value>(s, r, n1, n2, iwl, emit_at, after, g);
+    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto geo) {
+        surface_step<T, decltype(kind)::value, decltype(geo)::value>(s, r, n1, n2, iwl, emit_at, after, g);
     });
 }
 
@@ -1292,7 +1397,14 @@ inline DevSurface<double> lower_surface(const rtpb_surface& s) {
     if (d.kind == FLAT) axial = on_axis && z_axis(s.normal) && z_axis(s.input_axis);
     else if (d.kind == SPHERE) axial = on_axis && z_axis(s.input_axis) && d.shell_hi < HUGE_VAL;
     else if (d.kind == PERFECT_LENS) axial = on_axis && z_axis(s.normal);
-    if (axial) d.rcp_ok |= kAxial;
+    if (axial) {
+        d.rcp_ok |= kAxial;
+    } else {
+        // x-z plane geometry: every vector and point the step reads has an exact +0 y component (a flat's input axis
+        // drives its front-side test; a PerfectLens has none)
+        const bool y0 = is_p0(s.center[1]) && is_p0(s.normal[1]);
+        if ((d.kind == FLAT && y0 && is_p0(s.input_axis[1])) || (d.kind == PERFECT_LENS && y0)) d.rcp_ok |= kPlaneXZ;
+    }
     if (d.kind == PERFECT_LENS && std::fabs(s.focal_len) >= 0x1p-80 && std::fabs(s.focal_len) < 0x1p120)
         d.rcp_ok |= kLensQ1;
     d.nr = 0.0;
@@ -1326,8 +1438,10 @@ inline void lower_surface_media(DevSurface<double>& d, const DevMaterial<double>
             d.ln1f = n1 * d.f;
             d.lph = n1 * n1 * d.f + n2 * n2 * d.f;
             auto is_p0 = [](double v) { return host::bits(v) == 0; };
-            const bool on_axis = is_p0(d.lF[0]) && is_p0(d.lF[1]) && is_p0(d.lB[0]) && is_p0(d.lB[1]);
-            if (!(d.rcp_ok & kAxial) || on_axis)
+            // the focal planes take the step's center form (lens_step: GF), so F and B must have its zeros
+            const bool in_xz = is_p0(d.lF[1]) && is_p0(d.lB[1]);
+            const bool on_axis = in_xz && is_p0(d.lF[0]) && is_p0(d.lB[0]);
+            if ((d.rcp_ok & kAxial) ? on_axis : (d.rcp_ok & kPlaneXZ) ? in_xz : true)
                 d.rcp_ok |= (m1.kind == VACUUM || m2.kind == VACUUM) ? kLensUniVac : kLensUni;
         }
     }

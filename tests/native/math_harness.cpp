@@ -91,7 +91,7 @@ extern "C" int harness_surface_flags(const rtpb_surface* s) { return lower_surfa
 // The spot sweep's shared first surface (surface_step_pair, rtpb_math.h) against two separate steps, on the host:
 // n rays through surface s at Snell ratios ra and rb (uniform media), kPosOnly semantics.  out: [n][4][6] -- the
 // pair's two rays, then the two separate steps' rays (x, y, z, dx, dy, dz each).
-template <int K, bool AX>
+template <int K, int AX>
 static void pair_vs_steps(const DevSurface<double>& base, double ra, double rb, const double* in, int64_t n,
                           double* out) {
     constexpr int kMode = kPosOnly | kUniMedia;
@@ -106,7 +106,7 @@ static void pair_vs_steps(const DevSurface<double>& base, double ra, double rb, 
         const Rcp<double> iwl = make_wl_rcp(r.wl);
         Ray<double> res[4];
         double rxy[3] = {r.x * r.x + r.y * r.y, r.x * r.x + r.y * r.y, r.x * r.x + r.y * r.y};
-        const bool carry = K == SPHERE && AX;
+        const bool carry = K == SPHERE && AX == kGeoAxial;
         surface_step_pair<double, K, AX, kMode>(da, r, 1.0, iwl, ra, rb, r.wl, res[0], res[1],
                                                 static_cast<GuardBranch*>(nullptr), carry ? &rxy[0] : nullptr);
         auto none = [](const Ray<double>&) {};
@@ -126,11 +126,54 @@ extern "C" int harness_pair_vs_steps(const rtpb_surface* s, double ra, double rb
     const DevSurface<double> d = lower_surface(*s);
     const bool ax = (d.rcp_ok & kAxial) != 0;
     if (d.kind == SPHERE) {
-        if (ax) pair_vs_steps<SPHERE, true>(d, ra, rb, in, n, out);
-        else pair_vs_steps<SPHERE, false>(d, ra, rb, in, n, out);
+        if (ax) pair_vs_steps<SPHERE, kGeoAxial>(d, ra, rb, in, n, out);
+        else pair_vs_steps<SPHERE, kGeoGeneral>(d, ra, rb, in, n, out);
     } else if (d.kind == FLAT) {
-        if (ax) pair_vs_steps<FLAT, true>(d, ra, rb, in, n, out);
-        else pair_vs_steps<FLAT, false>(d, ra, rb, in, n, out);
+        if (ax) pair_vs_steps<FLAT, kGeoAxial>(d, ra, rb, in, n, out);
+        else if (d.rcp_ok & kPlaneXZ) pair_vs_steps<FLAT, kGeoXZ>(d, ra, rb, in, n, out);
+        else pair_vs_steps<FLAT, kGeoGeneral>(d, ra, rb, in, n, out);
+    } else {
+        return -1;
+    }
+    return 0;
+}
+
+// A positions-only step (the spot sweep's kPosOnly | kUniMedia semantics: forward-root kill of kAxial spheres, no TIR
+// position fill, front-side test folded into the final kill) against the full step of the history kernels, on the
+// host: n rays through surface s at the uniform Snell ratio `ratio`.  out: [n][2][6] -- the positions-only ray, then
+// the full step's "after" ray (x, y, z, dx, dy, dz each).
+template <int K, int AX>
+static void pos_vs_full(DevSurface<double> d, double ratio, const double* in, int64_t n, double* out) {
+    d.nr = ratio;
+    d.rcp_ok |= 4;
+    for (int64_t i = 0; i < n; ++i) {
+        const double* a = in + 8 * i;
+        const Ray<double> r{a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]};
+        const Rcp<double> iwl = make_wl_rcp(r.wl);
+        auto none = [](const Ray<double>&) {};
+        Ray<double> res[2];
+        double rxy = r.x * r.x + r.y * r.y;
+        constexpr bool carry = K == SPHERE && AX == kGeoAxial;
+        surface_step<double, K, AX, kPosOnly | kUniMedia>(d, r, 1.0, 1.0, iwl, none, res[0],
+                                                           static_cast<GuardBranch*>(nullptr), carry ? &rxy : nullptr);
+        surface_step<double, K, AX, 0>(d, r, 1.0, 1.0, iwl, none, res[1]);
+        for (int k = 0; k < 2; ++k) {
+            double* o = out + (i * 2 + k) * 6;
+            o[0] = res[k].x; o[1] = res[k].y; o[2] = res[k].z; o[3] = res[k].dx; o[4] = res[k].dy; o[5] = res[k].dz;
+        }
+    }
+}
+
+extern "C" int harness_pos_vs_full(const rtpb_surface* s, double ratio, const double* in, int64_t n, double* out) {
+    const DevSurface<double> d = lower_surface(*s);
+    const bool ax = (d.rcp_ok & kAxial) != 0;
+    if (d.kind == SPHERE) {
+        if (ax) pos_vs_full<SPHERE, kGeoAxial>(d, ratio, in, n, out);
+        else pos_vs_full<SPHERE, kGeoGeneral>(d, ratio, in, n, out);
+    } else if (d.kind == FLAT) {
+        if (ax) pos_vs_full<FLAT, kGeoAxial>(d, ratio, in, n, out);
+        else if (d.rcp_ok & kPlaneXZ) pos_vs_full<FLAT, kGeoXZ>(d, ratio, in, n, out);
+        else pos_vs_full<FLAT, kGeoGeneral>(d, ratio, in, n, out);
     } else {
         return -1;
     }

@@ -20,6 +20,7 @@ from serialize import material_to_dict, surface_to_dict
 import systems
 
 K_AXIAL = 64
+K_PLANE_XZ = 4096
 SPECIAL = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 5e-324, 1e300, -1e-300])
 
 
@@ -34,11 +35,26 @@ def axial_lens_system():
                      [mat.Bk7(), mat.Constant(1.2), mat.Constant(1.4), mat.Vacuum()]), mat.Vacuum(), mat.Constant(1.0)
 
 
+def tilted_xz_system():
+    """Surfaces tilted in the x-z plane (kPlaneXZ): flats and PerfectLens steps with normals (-sin t, 0, cos t) and
+    centers off the axis in x, between Constant, Sellmeier and Vacuum media -- uniform-media lenses (F, B in the
+    plane: the focal planes' x-z center form) and a lens beside a Sellmeier glass (per-ray focal points)."""
+    def n(t):
+        return [-np.sin(t), 0.0, np.cos(t)]
+    return rt.System([rt.FlatSurface([0.3, 0, 0], n(0.2), 20),
+                      rt.PerfectLens(15, [0.5, 0, 10], n(0.3), 0.8),
+                      rt.FlatSurface([1.0, 0, 22], n(0.25), 40),
+                      rt.PerfectLens(-12, [-0.7, 0, 35], n(-0.4), 0.7),
+                      rt.FlatSurface([0.0, 0, 50], n(0.1), 60)],
+                     [mat.Constant(1.3), mat.Vacuum(), mat.Bk7(), mat.Constant(1.1)]), mat.Vacuum(), mat.Constant(1.0)
+
+
 CASES = {
     "c1": lambda: (lambda c: (c[0], c[2], c[3]))(systems.c1_plano_convex(rt, mat, nrays=3)),
     "c5": lambda: (systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)),
     "c4": lambda: (systems.c4_system(rt, mat), mat.Constant(systems.OPM_N1), mat.Vacuum()),
     "lens": axial_lens_system,
+    "xz": tilted_xz_system,
 }
 
 
@@ -90,7 +106,25 @@ def test_axial_flags_set_where_the_geometry_is_axial(name):
         if isinstance(s, rt.PlaneMirror):
             axial = False
         assert bool(f & K_AXIAL) == axial, (type(s).__name__, s.center, s.input_axis)
-    assert any(f & K_AXIAL for f in flags)
+    assert any(f & K_AXIAL for f in flags) or name == "xz"
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_plane_xz_flags_set_where_the_geometry_allows(name):
+    """kPlaneXZ (the x-z-plane steps, GEO = kGeoXZ): flats and PerfectLens surfaces that are not axial and whose
+    center, normal (and, for a flat, input axis) have y components exactly +0 -- C4's five surfaces behind the 30 deg
+    tilt (scripts/2022_01_25_ray_trace_ideal_opm.py:59-80)."""
+    system, m0, m1 = CASES[name]()
+    flags = surface_flags(lowered(system, m0, m1, adversarial_rays(10)))
+    p0 = lambda v: np.asarray(v, float).view(np.uint64)[1] == 0          # noqa: E731
+    for s, f in zip(system.surfaces, flags):
+        want = (not f & K_AXIAL and isinstance(s, (rt.FlatSurface, rt.PerfectLens)) and p0(s.center) and p0(s.normal)
+                and (isinstance(s, rt.PerfectLens) or p0(s.input_axis)))
+        assert bool(f & K_PLANE_XZ) == want, (type(s).__name__, s.center, s.normal)
+    if name == "c4":
+        assert sum(bool(f & K_PLANE_XZ) for f in flags) == 5
+    if name == "xz":
+        assert all(f & K_PLANE_XZ for f in flags)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))

@@ -91,7 +91,7 @@ def test_spot_sweep_matches_oracle_c5_small():
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
-@pytest.mark.parametrize("case", ["c5", "c5_bundles", "c2", "tir", "tir_last", "stress"])
+@pytest.mark.parametrize("case", ["c5", "c5_bundles", "c5_backward", "c2", "tir", "tir_last", "stress"])
 def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     """One-kernel sweep (generate + trace + reduce) == fan kernel + trace(planes='final') + spot stats,
     bit for bit, for a lens system (C5) and a lens-free one (C2), in both storage types; several
@@ -110,6 +110,13 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
         system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
         fields, wls, theta = systems.c5_field_points(2), list(np.linspace(0.4, 0.8, 9)), 0.5 * np.pi / 180
         gpb = 13
+    elif case == "c5_backward":
+        # field points inside the first sphere's ball (forward roots on its far side, u2 < 0), in the glass between
+        # surfaces, and beyond the whole system (both roots of every sphere behind the rays): the sweep's forward-root
+        # kill and one-compare discriminant guard against the full-semantics trace
+        system, m0, m1 = systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1)
+        fields, wls, theta = [[0.0, 0.0, 195.0], [0.7, -0.4, 250.0], [1.0, 0.5, 2500.0], [0.0, 0.0, 0.0]], \
+            [0.405, 0.532, 0.785], 0.6
     elif case == "c2":
         system, m0, m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
         fields, wls, theta = [[0.0, 0.0, -5.0], [1.0, -2.0, -5.0]], list(systems.C2_WAVELENGTHS), 0.05
@@ -127,9 +134,12 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     assert fu.keys() == un.keys()
     for k in fu:
         assert same_bits(fu[k], un[k]), k
-    assert fu["count"].min() > 0
+    if case != "c5_backward":
+        assert fu["count"].min() > 0
     if case not in ("c5", "c5_bundles", "c2"):
         assert (fu["count"] < 301 * 77).any()            # some rays of the bundle are lost on the way
+    if case == "c5_backward":
+        assert (fu["count"] == 0).any()                  # the field beyond the system: every row killed
 
 
 @pytest.mark.parametrize("case", ["astig_relay", "reversed_doublet", "fuzz_01", "fuzz_03", "fuzz_06", "fuzz_13",

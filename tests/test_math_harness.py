@@ -135,6 +135,43 @@ def test_sweep_pair_step_equals_two_steps(name):
     assert tried > 0
 
 
+@pytest.mark.parametrize("name", ["c5_odt", "c3_relay", "c2_achromat", "stress", "fuzz_03", "fuzz_23"])
+def test_positions_only_step_matches_the_full_step(name):
+    """The spot sweep's positions-only steps (kPosOnly: a kAxial sphere's backward or infinite root kills the row
+    instead of becoming a NaN t, no TIR position fill, the front-side test joined to the final kill) leave every live
+    row of the full step bit for bit (positions and directions) and a NaN direction on every other row -- the
+    final-position semantics the sweep's reduction applies.  Rays: the golden bundle, the same rays reversed (both
+    roots behind them), started from inside the spheres' balls and beyond the system, and adversarial components."""
+    import json
+    import systems
+    lib = harness()
+    fn = lib.harness_pos_vs_full
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    spec, rays, _ = load_case(name)
+    system, m0, m1 = system_from_json(rt, mat, json.dumps(spec))
+    back = rays.copy()
+    back[:, 3:6] *= -1
+    deep = rays.copy()
+    deep[:, 2] += np.linspace(0.0, 3000.0, rays.shape[0])           # from the front of the system to far beyond it
+    rays = np.concatenate([rays, back, deep, systems.stress_rays(256, seed=5)], axis=0)
+    low = E.lower(system.surfaces, [m0] + list(system.materials) + [m1], lambda: np.unique(rays[:, 7]), C.RTPB_F64)
+    tried = killed = 0
+    for k in range(low.nsurf):
+        if low.surfaces[k].kind not in (C.RTPB_FLAT, C.RTPB_SPHERE) or not isinstance(
+                system.surfaces[k], rt.RefractingSurface):
+            continue
+        x = np.ascontiguousarray(rays, dtype=np.float64)
+        out = np.empty((x.shape[0], 2, 6))
+        assert fn(ctypes.byref(low.surfaces[k]), 1.0 / 1.5, x.ctypes.data, x.shape[0], out.ctypes.data) == 0
+        live = ~np.isnan(out[:, 1, 3])
+        assert same_bits(out[live, 0], out[live, 1]), (name, k)
+        assert np.isnan(out[~live, 0, 3]).all(), (name, k)
+        tried += 1
+        killed += int((~live).sum())
+    assert tried > 0 and killed > 0
+
+
 def test_sweep_fan_index_division_is_exact():
     """rtpb_spot_sweep divides the fan index j by n_thetas as (j * mul) >> shift (rtpb_math.h sweep_divisor):
     exact for every j < 2^31 -- checked at the quotient boundaries (multiples of d and their neighbours), near 2^31
