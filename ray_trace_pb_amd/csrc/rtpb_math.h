@@ -777,6 +777,20 @@ RTPB_HD int32_t bit_select(int32_t mask, int32_t a, int32_t b) {
 #endif
 }
 
+// a * B for |a| < 2^23 and a small constant B (v_mul_i32_i24 with an inline constant: one VALU where the compiler,
+// not knowing the range, emits two)
+template <int B>
+RTPB_HD int32_t mul_i24(int32_t a) {
+    static_assert(B >= -16 && B <= 64, "inline constant");
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "i"(B));
+    return r;
+#else
+    return a * B;
+#endif
+}
+
 // A nearly unit vector over its norm, NaN components replaced by 0: nc = N x nb (RT:1207-1209), with N a unit normal
 // and nb a unit tangent, has |nc|^2 = |N|^2 |nb|^2 - (N . nb)^2 within a few ulps of 1 on every live row away from
 // normal incidence.  For |v - 1| <= 2^-31 the square root and the reciprocal the quotients need are read off the
@@ -795,10 +809,11 @@ RTPB_HD void unit_near1_or_zero(T& x, T& y, T& z, G* g = nullptr) {
         if (__builtin_expect(tabs<T>(v - T(1)) <= T(0x1p-31), 1)) {      // v - 1 is exact (Sterbenz); NaN fails
             const int32_t d = __double2loint(v);
             const int32_t neg = d >> 31;                                // -1 where v < 1
-            // the reciprocal's offset, m >= 0 ? -2m : ceil(-m / 2) with m = d >> 1, in terms of d and as a bit select:
-            // d >= 0 ? -(d & ~1) : (3 - d) >> 2
-            const int32_t t = bit_select(neg, (3 - d) >> 2, -(d & ~1));
-            const double s = __hiloint2double(__double2hiint(v), d >> 1);   // hi(v) = 0x3FF00000 + neg here
+            const int32_t m = d >> 1;
+            // the reciprocal's offset, m >= 0 ? -2m : ceil(-m / 2) = (1 - m) >> 1, as a bit select; -2m as one 24-bit
+            // multiply (|m| <= 2^21 inside the window)
+            const int32_t t = bit_select(neg, (1 - m) >> 1, mul_i24<-2>(m));
+            const double s = __hiloint2double(__double2hiint(v), m);    // hi(v) = 0x3FF00000 + neg here
             const double yr = __hiloint2double(0x3FF00000 + (t >> 31), t);
             div3_norm<T, G, 1>(x, y, z, Rcp<T>{s, yr, true, T(0)}, g);   // components at most ~1: no fixup
             return;
