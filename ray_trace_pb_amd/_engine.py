@@ -835,6 +835,21 @@ def check_out(out, shape, dtype, device):
     return out
 
 
+_STREAMS = {}               # (device, raw hipStream_t) -> torch.cuda.Stream of torch's current stream
+
+
+def _raw_stream(dev):
+    """torch's current raw hipStream_t on device `dev` (torch._C._cuda_getCurrentRawStream: no Stream wrapper)."""
+    global _raw_stream
+    import torch
+    get = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if get is None:
+        def get(d):
+            return torch.cuda.current_stream(d).cuda_stream
+    _raw_stream = get
+    return get(dev)
+
+
 def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None, miss=None, own_out=False):
     """torch CUDA (N, 8) -> torch CUDA (len(planes), N, 8) [AOS] or (len(planes), 8, N) [SOA] of the
     plan's storage type.  ``miss``: a zeroed int32 CUDA tensor the launch sets to 1 when a ray's
@@ -848,28 +863,41 @@ def trace_device(low, rays, planes, layout_out=C.RTPB_AOS, out=None, stream=None
     if rays.dtype != want or not rays.is_contiguous():
         rays = rays.to(dtype=want).contiguous()
     n = rays.shape[0]
+    dev = rays.get_device()
     fresh_out = (out is None or own_out) and stream is None
     if out is None:
         shape = (len(planes), n, 8) if layout_out == C.RTPB_AOS else (len(planes), 8, n)
         out = device_empty(shape, tdt, rays.device)
     lo, hi = plane_mask(planes)
     if stream is None:
-        cur = torch.cuda.current_stream(rays.device)
-        stream = cur.cuda_stream
+        # torch's current stream: its raw handle, and one torch.cuda.Stream per handle (the wrapper record_stream
+        # takes) instead of a new wrapper per call
+        stream = _raw_stream(dev)
+        cur = _STREAMS.get((dev, stream))
+        if cur is None:
+            cur = torch.cuda.current_stream(dev)
+            if len(_STREAMS) > 64:
+                _STREAMS.clear()
+            _STREAMS[(dev, stream)] = cur
     elif isinstance(stream, torch.cuda.Stream):
         cur, stream = stream, stream.cuda_stream
     else:
         # a raw hipStream_t: torch's view of it, so the launch's use can be recorded
-        cur = torch.cuda.ExternalStream(stream, device=rays.device)
+        cur = _STREAMS.get((dev, stream))
+        if cur is None:
+            cur = torch.cuda.ExternalStream(stream, device=rays.device)
+            if len(_STREAMS) > 64:
+                _STREAMS.clear()
+            _STREAMS[(dev, stream)] = cur
     lib = C.lib()
     p = _acquire(low)
     try:
         if miss is None:
-            rc = lib.rtpb_trace(p.ptr, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0,
-                                out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream)
+            rc = lib.rtpb_trace(p.ptr, dev, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0, out.data_ptr(), layout_out,
+                                8 * n, n, lo, hi, stream)
         else:
-            rc = lib.rtpb_trace_checked(p.ptr, rays.device.index or 0, rays.data_ptr(), in_code, n, C.RTPB_AOS,
-                                        0, out.data_ptr(), layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr())
+            rc = lib.rtpb_trace_checked(p.ptr, dev, rays.data_ptr(), in_code, n, C.RTPB_AOS, 0, out.data_ptr(),
+                                        layout_out, 8 * n, n, lo, hi, stream, miss.data_ptr())
     finally:
         _release(p)
     if rc:

@@ -495,3 +495,32 @@ def test_trim_allocate_cycles_grow_dead_va_by_one_segment_each():
     assert all(d == steps[0] for d in steps) and steps[0] >= 4 << 30 and steps[0] <= seg
     limit = E.buffer_stats()["dead_va_limit"]
     assert limit // (19 * 50_007_030 * 8 * 4) >= 1000
+
+
+@pytest.mark.skipif(not _sleep_available(), reason="torch.cuda._sleep is not available")
+def test_trace_on_a_raw_stream_is_recorded_with_torch():
+    """trace_device with an explicit raw hipStream_t records its use of `out` and of the rays with torch
+    (through torch.cuda.ExternalStream): a torch history traced on a delayed side stream and freed at once is not
+    handed to the next allocation of its size before that trace has run -- which then reads back bitwise."""
+    from ray_trace_pb_amd import _engine as E
+    system, m0, m1, rays, ref = golden("c3_relay")
+    mats = [m0] + list(system.materials) + [m1]
+    low = E.lower(system.surfaces, mats, lambda: np.unique(rays[:, 7]), C.RTPB_F64)
+    x = torch.from_numpy(rays).to(DEV)
+    planes = E.resolve_planes("all", len(system.surfaces))
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    out = torch.empty(ref.shape, dtype=torch.float64, device=DEV)       # torch's default pool, current stream
+    p = out.data_ptr()
+    _delay(side, 300_000_000)
+    E.trace_device(low, x, planes, out=out, stream=side.cuda_stream)     # raw handle
+    host = torch.empty(ref.shape, dtype=torch.float64, pin_memory=True)
+    with torch.cuda.stream(side):
+        host.copy_(out, non_blocking=True)
+    del out
+    gc.collect()
+    nxt = torch.empty(ref.shape, dtype=torch.float64, device=DEV)
+    assert nxt.data_ptr() != p                                          # the pending trace's block was withheld
+    nxt.fill_(-1.0)
+    torch.cuda.synchronize()
+    assert same_bits(host.numpy(), ref)

@@ -64,7 +64,9 @@ def run(out, config, scale):
     prev = 0.0
     for k in range(1, S + 1):
         s = system.surfaces[k - 1]
-        ax = "axial" if (tuple(s.input_axis) == (0.0, 0.0, 1.0) and s.center[0] == 0 and s.center[1] == 0) else "general"
+        ax = ("axial" if (tuple(s.input_axis) == (0.0, 0.0, 1.0) and s.center[0] == 0 and s.center[1] == 0) else
+              "x-z" if (float(s.center[1]) == 0 and float(getattr(s, "normal", s.input_axis)[1]) == 0
+                        and not isinstance(s, rt.SphericalSurface)) else "general")
         print(f"surface {k - 1:2d} {type(s).__name__:17s} {ax:8s} VALU per ray {per_ray[k] - prev:7.1f}  "
               f"(cumulative {per_ray[k]:8.1f})", flush=True)
         prev = per_ray[k]
