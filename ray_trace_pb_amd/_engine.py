@@ -112,7 +112,12 @@ _CALLS_MAX = 16
 
 
 class _Call:
-    __slots__ = ("surfaces", "items", "materials", "dtype", "gen", "arrays", "blob", "low")
+    __slots__ = ("surfaces", "items", "materials", "dtype", "gen", "arrays", "blob", "low", "lists", "keys_gen")
+
+
+# bumped whenever remember_keys changes the key set of some tabulated materials: a memoised lowering of a tabulated
+# system holds the keys of its time and is valid only while this is unchanged
+KEYS_GEN = [0]
 
 
 _SCALAR_ATTRS = ("aperture_rad", "radius", "focal_len", "alpha")
@@ -146,30 +151,57 @@ def _call_arrays(surfaces):
 
 
 def memo_lookup(surfaces, materials, dtype):
-    """The lowering of the previous call with these very surface and material objects, if provably unchanged."""
+    """(lowering, tabulated) of the previous call with these very surface and material objects, if provably
+    unchanged -- a tabulated system's lowering holds the table keys of the previous bundle (valid while KEYS_GEN is
+    unchanged; the caller still checks the bundle against them) -- or None."""
     e = _CALLS.get(id(surfaces))
     if e is None or e.surfaces is not surfaces or e.gen != MUTATIONS[0] or e.dtype != dtype:
+        return None
+    if e.keys_gen is not None and e.keys_gen != KEYS_GEN[0]:
         return None
     if e.items != surfaces or e.materials != materials:
         return None
     if b"".join([a.tobytes() for a in e.arrays]) != e.blob:
         return None
-    return e.low
+    for lst, snap in e.lists:
+        if tuple(lst) != snap:
+            return None
+    return e.low, e.keys_gen is not None
 
 
-def memo_store(surfaces, materials, dtype, low):
-    """Remember ``low`` as the lowering of (surfaces, materials, dtype) for memo_lookup (untabulated systems)."""
+def _material_lists(materials):
+    """Snapshots of the list attributes (of plain numbers) of the materials (Ebaf11.params: editable in place), or None
+    when some attribute is neither a number, a string, None nor such a list."""
+    lists = []
+    for m in materials:
+        for v in vars(m).values():
+            if v is None or isinstance(v, (str,) + _NUMBER):
+                continue
+            if isinstance(v, list) and all(isinstance(x, _NUMBER) for x in v):
+                lists.append((v, tuple(v)))
+                continue
+            return None
+    return lists
+
+
+def memo_store(surfaces, materials, dtype, low, tabulated=False):
+    """Remember ``low`` as the lowering of (surfaces, materials, dtype) for memo_lookup.  ``tabulated``: lowered with
+    the previous bundle's table keys (valid while KEYS_GEN is unchanged); every tabulated material must have a pure
+    n() (the package's own, or ``rtpb_pure_n``)."""
     if not isinstance(surfaces, list):
         return
     arrs = _call_arrays(surfaces)
     if arrs is None:
         return
-    for m in materials:
-        if not all(isinstance(v, _NUMBER) for v in vars(m).values() if v is not None and not isinstance(v, str)):
-            return
+    lists = _material_lists(materials)
+    if lists is None:
+        return
+    if tabulated and not all(_pure_n(m) for m in tabulated_materials(materials)):
+        return
     e = _Call()
     e.surfaces, e.items, e.materials, e.dtype = surfaces, list(surfaces), list(materials), dtype
     e.gen, e.arrays, e.blob, e.low = MUTATIONS[0], arrs, b"".join([a.tobytes() for a in arrs]), low
+    e.lists, e.keys_gen = lists, (KEYS_GEN[0] if tabulated else None)
     with _memo_lock:
         _CALLS[id(surfaces)] = e
         _CALLS.move_to_end(id(surfaces))
@@ -339,6 +371,9 @@ def tabulated(materials):
     return [m for m in materials if not (hasattr(m, "_rtpb_lower") and m._rtpb_lower() is not None)]
 
 
+tabulated_materials = tabulated
+
+
 def table_fingerprint(materials):
     """Hashable identity of the tabulated materials' n() (class + attribute values), or None.  A material
     may supply ``_rtpb_table_key()`` (a cheap hashable of everything its n() reads; Ebaf11 does)."""
@@ -360,6 +395,7 @@ def previous_keys(fp):
 
 
 def remember_keys(fp, keys):
+    KEYS_GEN[0] += 1
     if fp is None:
         return
     with _memo_lock:

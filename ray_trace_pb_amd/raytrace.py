@@ -568,22 +568,37 @@ def _trace_device_tables(surfaces, materials, rays, last, code, sel, extend, lay
         dst = _default_history(code, last, sel, layout_code)
         return E.trace_device(low, last, sel, layout_out=layout_code, miss=miss, out=dst, own_out=dst is not None)
 
-    low = E.memo_lookup(surfaces, materials, code)
-    if low is not None:
-        return run(low)
+    def run_checked(low):
+        """The launch with the table-miss flag; None when some ray's wavelength is not a key of the tables."""
+        miss = _miss_flag(last.device)
+        miss[0] = 0
+        res = run(low, miss)
+        torch.cuda.current_stream(last.device).synchronize()       # the launch has set the flag or not
+        return res if int(miss[0]) == 0 else None
+
+    memo = E.memo_lookup(surfaces, materials, code)
+    missed = False
+    if memo is not None:
+        low, with_keys = memo
+        if not with_keys:
+            return run(low)
+        res = run_checked(low)                 # the previous bundle's keys, memoised with the lowering
+        if res is not None:
+            return res
+        del res
+        missed = True                          # those keys miss a ray: straight to the bundle's own keys
     tab = E.tabulated(materials)
     if not tab:
         low = E.lower(surfaces, materials, None, code, tab=tab)
         E.memo_store(surfaces, materials, code, low)
         return run(low)
     fp = E.table_fingerprint(tab)
-    prev = E.previous_keys(fp)
+    prev = None if missed else E.previous_keys(fp)
     if prev is not None:
-        miss = _miss_flag(last.device)
-        miss[0] = 0
-        res = run(E.lower(surfaces, materials, lambda: prev, code), miss)
-        torch.cuda.current_stream(last.device).synchronize()       # the launch has set the flag or not
-        if int(miss[0]) == 0:
+        low = E.lower(surfaces, materials, lambda: prev, code)
+        res = run_checked(low)
+        if res is not None:
+            E.memo_store(surfaces, materials, code, low, tabulated=True)
             return res
         del res
     keys = E.distinct_wavelengths(last[:, 7])

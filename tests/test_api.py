@@ -289,6 +289,11 @@ def test_lowering_memo_follows_in_place_changes():
     assert E.lower(system.surfaces, mats, None, C.RTPB_F64) is low0
 
 
+def _memo_low(*args):
+    r = E.memo_lookup(*args)
+    return None if r is None else r[0]
+
+
 def test_call_memo_follows_every_change():
     """The drop-in call's memo (a repeated System.ray_trace skips the content key) returns the
     previous lowering only while nothing it read can have changed: in-place array edits, attribute rebinding on a
@@ -301,29 +306,49 @@ def test_call_memo_follows_every_change():
         return [m0] + list(system.materials) + [m1]
     low = E.lower(system.surfaces, mats(), None, C.RTPB_F64)
     E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F32) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is low
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F32) is None
     z0 = system.surfaces[-1].center[2]
     system.surfaces[-1].center[2] = z0 + 1.0                      # in place: the bytes differ
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None
     system.surfaces[-1].center[2] = z0
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is low
     system.surfaces[-1].normal[2] = system.surfaces[-1].normal[2]     # an int64 normal array, unchanged bytes
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is low
     sph = system.surfaces[1]
     sph.radius = sph.radius                                          # any rebinding counts
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None
     E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
     m0.b1 = m0.b1                                                    # a material attribute
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None
     E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
-    assert E.memo_lookup(system.surfaces, [mat.Vacuum()] + mats()[1:], C.RTPB_F64) is None   # another medium
+    assert _memo_low(system.surfaces, [mat.Vacuum()] + mats()[1:], C.RTPB_F64) is None   # another medium
     old = system.surfaces[0]
     system.surfaces[0] = rt.FlatSurface(old.center, old.normal, old.aperture_rad)            # another surface
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None
     system.surfaces[0] = old
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None    # (constructing a surface counted too)
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None    # (constructing a surface counted too)
     E.memo_store(system.surfaces, mats(), C.RTPB_F64, low)
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is low
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is low
     del sph.radius                                                   # deletion counts too
-    assert E.memo_lookup(system.surfaces, mats(), C.RTPB_F64) is None
+    assert _memo_low(system.surfaces, mats(), C.RTPB_F64) is None
+
+
+def test_call_memo_of_tabulated_systems():
+    """A tabulated system's memo (Ebaf11: the previous bundle's table keys, still checked by the kernel's table-miss
+    flag) holds only while the key sets are unchanged (any remember_keys) and the material's coefficient list is
+    unchanged in place."""
+    system = systems.c3_system(rt, mat)
+    m0 = m1 = mat.Vacuum()
+    mats = [m0] + list(system.materials) + [m1]
+    eb = next(m for m in mats if type(m).__name__ == "Ebaf11")
+    low = E.lower(system.surfaces, mats, lambda: np.array([0.635]), C.RTPB_F32)
+    E.memo_store(system.surfaces, mats, C.RTPB_F32, low, tabulated=True)
+    assert E.memo_lookup(system.surfaces, mats, C.RTPB_F32) == (low, True)
+    p0 = eb.params[0]
+    eb.params[0] = p0 * 1.001                                    # in place: no __setattr__
+    assert E.memo_lookup(system.surfaces, mats, C.RTPB_F32) is None
+    eb.params[0] = p0
+    assert E.memo_lookup(system.surfaces, mats, C.RTPB_F32) == (low, True)
+    E.remember_keys(None, np.array([0.5]))                     # some key set changed
+    assert E.memo_lookup(system.surfaces, mats, C.RTPB_F32) is None
