@@ -91,6 +91,7 @@ def parse():
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow --gpus N above the visible GPU count (ranks share GPUs: a rehearsal, not a measurement)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-shard", default="0,1", help=argparse.SUPPRESS)       # rank,world of a c4 PMC child
     return ap.parse_args()
 
 
@@ -414,9 +415,10 @@ def cpu_parallel(config, procs, secs=4.0):
 
 
 # ---------------------------------------------------------------------------------------------- PMC
-def _pmc_run(args, config, counters, kernel):
+def _pmc_run(args, config, counters, kernel, shard=(0, 1)):
     """One rocprofv3 --pmc child run of this script (--pmc-child --config CONFIG): per-dispatch counter
-    values of the kernels whose name contains `kernel` -> {counter: [values]} or an error string."""
+    values of the kernels whose name contains `kernel` -> {counter: [values]} or an error string.  `shard`: the
+    (rank, world) whose C4 shard the child traces (the child runs on the calling rank's GPU)."""
     import csv
     prof = shutil.which("rocprofv3")
     if not prof:
@@ -426,7 +428,7 @@ def _pmc_run(args, config, counters, kernel):
     cmd = [prof, "--pmc"] + list(counters) + ["--output-format", "csv", "-d", d, "-o", "pmc", "--",
                                               sys.executable, os.path.abspath(__file__), "--pmc-child",
                                               "--config", config, "--scale", str(args.scale), "--rays",
-                                              str(args.rays)]
+                                              str(args.rays), "--pmc-shard", f"{shard[0]},{shard[1]}"]
     try:
         subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                        stdin=subprocess.DEVNULL, env=dict(os.environ, TMPDIR="/tmp"))
@@ -445,13 +447,13 @@ def _pmc_run(args, config, counters, kernel):
     return vals, None
 
 
-def measure_traffic(args, config):
+def measure_traffic(args, config, shard=(0, 1)):
     """HBM bytes per trace launch from rocprofv3 PMC counters (FETCH_SIZE and WRITE_SIZE in separate
     passes; gfx950: FETCH_SIZE counts half the bytes of wide streaming reads, so it is doubled --
-    MI355X_MICROARCH.md §HBM).  Counters are in KiB."""
+    MI355X_MICROARCH.md §HBM).  Counters are in KiB.  `shard`: C4's (rank, world) shard."""
     out = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        vals, err = _pmc_run(args, config, [ctr], "trace_kernel")
+        vals, err = _pmc_run(args, config, [ctr], "trace_kernel", shard)
         if err:
             return None, err
         out[ctr] = float(np.median(vals[ctr]))
@@ -628,8 +630,9 @@ def run_c4(args, dev, rank, world, copy):
     res = None
     if rank == 0:
         traffic, note = (None, None)
-        if world == 1 and args.traffic == "auto":
-            traffic, note = measure_traffic(args, "c4")
+        if args.traffic == "auto":
+            # N > 1: rank 0's own shard, in child runs on its GPU (the other ranks wait at the next barrier)
+            traffic, note = measure_traffic(args, "c4", (rank, world))
         per_rank = [{"rank": r, "rays": int(x[2]), "kernel_ms": x[1],
                      "alg_GBps": x[2] * wl.bytes_per_ray / (x[1] * 1e-3) / 1e9,
                      "frac_8TBs": x[2] * wl.bytes_per_ray / (x[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, "wall_s": x[0]}
@@ -641,6 +644,8 @@ def run_c4(args, dev, rank, world, copy):
                "parallelism": f"phi-row ray shards x{world} (no collective)",
                "roofline": roofline(wl, max(x[1] for x in g), traffic, note, wl.fill_rate() if world == 1 else None,
                                     copy),
+               "roofline_scope": "per GPU: rank 0's shard bytes over the slowest rank's kernel time" if world > 1
+                                 else "the whole fan on one GPU",
                "per_rank": per_rank}
         if world == 1:
             res["roofline"]["note"] = "N=1: the whole 100M-ray fan on one GPU (80 GB in HBM)"
@@ -717,7 +722,9 @@ def run_c5(args, dev, rank, world):
     rl = {"bound": "valu_f64", "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "sweep_kernel",
           "kernel_ms_max_rank": kmax, "hbm_GBps_max_rank": max(p["hbm_GBps"] for p in per_rank),
           "hbm_note": "the rays never leave registers: HBM carries only the per-tile partial sums"}
-    if world == 1 and args.traffic == "auto":
+    if args.traffic == "auto":
+        # N > 1: the per-ray counts of a 1-field sample on rank 0's GPU (the sweep's work per ray does not depend on
+        # the field split); achieved / frac are then per GPU (rank 0's rays over its kernel time)
         fl, err = measure_c5_flops(args)
         if fl:
             rays0 = g[0][2]
@@ -751,6 +758,7 @@ def run_c5(args, dev, rank, world):
                                     "4) and a float64 transcendental at 2.97x (tools/valu/valu_rates.hip), over 1024 "
                                     "SIMDs at 2.4 GHz; frac_issue = that ceiling / the measured kernel time"))
             rl["frac"] = rl["achieved"] / F64_VALU_PEAK_TFLOPS
+            rl["scope"] = "per GPU: rank 0's rays over its kernel time" if world > 1 else "one GPU"
             rl["frac_effective"] = rl["achieved_effective"] / F64_VALU_PEAK_TFLOPS
         else:
             rl["flops_note"] = err
@@ -771,7 +779,8 @@ def pmc_child(args, dev):
         analysis.spot_sweep(systems.c5_system(rt, mat), mat.Constant(1), mat.Constant(1),
                             systems.c5_field_points(8)[:1], wls, 0.5 * np.pi / 180, C5_FAN[0], C5_FAN[1], device=dev)
     else:
-        wl = Workload(args.config, dev, 0, scale=args.scale, c2_rays=args.rays)
+        r, w = (int(v) for v in args.pmc_shard.split(","))
+        wl = Workload(args.config, dev, r, world=w, scale=args.scale, c2_rays=args.rays)
         for _ in range(3):
             wl.step()
     torch.cuda.synchronize()

@@ -91,7 +91,7 @@ def test_spot_sweep_matches_oracle_c5_small():
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
-@pytest.mark.parametrize("case", ["c5", "c5_bundles", "c5_backward", "c2", "tir", "tir_last", "stress"])
+@pytest.mark.parametrize("case", ["c5", "c5_bundles", "c5_backward", "c2", "tir", "tir_last", "stress", "c4", "xz"])
 def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     """One-kernel sweep (generate + trace + reduce) == fan kernel + trace(planes='final') + spot stats,
     bit for bit, for a lens system (C5) and a lens-free one (C2), in both storage types; several
@@ -120,6 +120,16 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
     elif case == "c2":
         system, m0, m1 = systems.c2_system(rt, mat), mat.Vacuum(), mat.Vacuum()
         fields, wls, theta = [[0.0, 0.0, -5.0], [1.0, -2.0, -5.0]], list(systems.C2_WAVELENGTHS), 0.05
+    elif case == "c4":
+        # the OPM: axial lenses and flats, then five surfaces in the x-z plane (kPlaneXZ) behind the 30 deg tilt
+        system, m0, m1 = systems.c4_system(rt, mat), mat.Constant(systems.OPM_N1), mat.Vacuum()
+        fields, wls, theta = [[1e-3, 1e-3, 1e-3 * np.tan(np.pi / 6)], [0.0, 0.0, 0.0]], \
+            [systems.OPM_WAVELENGTH, 0.9 * systems.OPM_WAVELENGTH], np.arcsin(1.35 / systems.OPM_N1)
+    elif case == "xz":
+        # tilted flats and PerfectLens steps in the x-z plane, Constant / Sellmeier / Vacuum media (test_axial.py)
+        from test_axial import tilted_xz_system
+        system, m0, m1 = tilted_xz_system()
+        fields, wls, theta = [[0.0, 0.0, -3.0], [0.4, -0.3, -3.0]], [0.5, 0.6], 0.2
     elif case in ("tir", "tir_last"):
         system, _, m0, m1 = systems.tir_prism(rt, mat)
         if case == "tir_last":
@@ -136,7 +146,7 @@ def test_fused_spot_sweep_bitwise_equals_unfused(case, dtype):
         assert same_bits(fu[k], un[k]), k
     if case != "c5_backward":
         assert fu["count"].min() > 0
-    if case not in ("c5", "c5_bundles", "c2"):
+    if case not in ("c5", "c5_bundles", "c2", "xz"):
         assert (fu["count"] < 301 * 77).any()            # some rays of the bundle are lost on the way
     if case == "c5_backward":
         assert (fu["count"] == 0).any()                  # the field beyond the system: every row killed
