@@ -880,6 +880,8 @@ class System:
         classes = tuple(map(type, self.surfaces))
         custom = _CUSTOM.get(classes)
         if custom is None:
+            if len(_CUSTOM) > 256:
+                _CUSTOM.clear()
             custom = _CUSTOM[classes] = [s._rtpb_user_propagate() or s._rtpb_user_geometry() for s in self.surfaces]
         if not any(custom):
             return trace_surfaces(self.surfaces, materials, rays, planes=planes, dtype=dtype, devices=devices,

@@ -12,6 +12,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py --steps 20 --warmup 5 (the bench line; PMC traffic child runs included)
 #   bench2           the N>1 path rehearsed: python bench.py --gpus 2 --oversubscribe (2 ranks, one GPU)
+#   bench2pmc        the same with rank 0's PMC child runs (C4 traffic of its shard, C5 FLOP roofline)
 #   rocprof          rocprofv3 --kernel-trace --stats of the headline loop alone (--extras off: the csv
 #                    average is the timed launches' average) + the timed-launch split
 #   pmc_c3|pmc_c4    PMC passes (tools/pmc_kernel.sh) of the C3 / C4 history kernel
@@ -55,6 +56,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py --steps 20 --warmup 5 ;;
     bench2) step bench2 900 python bench.py --gpus 2 --oversubscribe --steps 20 --warmup 3 --cpu-baseline off --traffic off ;;
+    bench2pmc) step bench2pmc 900 python bench.py --gpus 2 --oversubscribe --steps 10 --warmup 3 --cpu-baseline off ;;
     rocprof)
       step rocprof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/rocprof" -o c3 -- \
         python3 bench.py --configs none --extras off --cpu-baseline off --traffic off --steps 20 --warmup 5

@@ -3,6 +3,7 @@
 
     python tools/isa_compare.py dump DIR          # write DIR/<source>.s
     python tools/isa_compare.py compare DIR_A DIR_B
+    python tools/isa_compare.py valu DIR_A DIR_B [REGEX]   # static VALU instruction counts per function
 """
 import concurrent.futures
 import glob
@@ -73,8 +74,25 @@ def compare(a, b):
     return not diff
 
 
+def valu(a, b, pattern="."):
+    """Static VALU instruction counts of the functions matching `pattern` in two dumps (code size, not the
+    executed count: tools/history_kind_cost.py and the PMC passes measure that)."""
+    def counts(d):
+        out = {}
+        for p in glob.glob(os.path.join(d, "*.s")):
+            for k, body in functions(p).items():
+                if re.search(pattern, k):
+                    out[k] = sum(1 for ln in body.splitlines() if ln.strip().startswith("v_"))
+        return out
+    ca, cb = counts(a), counts(b)
+    for k in sorted(set(ca) | set(cb)):
+        print(f"{ca.get(k, '-'):>7} {cb.get(k, '-'):>7}  {k[:140]}")
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "dump":
         dump(sys.argv[2])
+    elif sys.argv[1] == "valu":
+        valu(*sys.argv[2:5])
     else:
         sys.exit(0 if compare(sys.argv[2], sys.argv[3]) else 1)
