@@ -278,6 +278,20 @@ constexpr int kGeoXZ = 2;          // kPlaneXZ: normal, input axis and center wi
 
 RTPB_HD double tfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// +0 as an operand the compiler cannot see is zero: fma(-a, 0, b) with a visible zero is rewritten to
+// fma(a, -0, b), and -0 is no inline constant of gfx950, so the product needs the two-address fmac with a
+// literal (plus a register copy wherever b stays live).  With the zero in a scalar register the negation stays a
+// source modifier of one three-address v_fma_f64.  Same operation, same bits.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double zero_s() {
+    double z;
+    asm("s_mov_b64 %0, 0" : "=s"(z));
+    return z;
+}
+#else
+inline double zero_s() { return 0.0; }
+#endif
+
 // v . n for a surface vector n; kGeoAxial: n == (+0, +0, 1); kGeoXZ: ny == +0
 template <int GEO, typename T>
 RTPB_HD T axdot(T vx, T vy, T vz, T nx, T ny, T nz) {
@@ -830,7 +844,7 @@ template <int GEO = kGeoGeneral, typename T, class G = GuardBranch>
 RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& cz, G* g = nullptr) {
     T bx, by, bz;
     if constexpr (GEO == kGeoAxial) {
-        bx = tfma(-ri.dz, T(0), ri.dy);                   // dy * 1 - dz * 0
+        bx = tfma(-ri.dz, zero_s(), ri.dy);               // dy * 1 - dz * 0
         by = tfma(ri.dz, T(0), -ri.dx);                   // dz * 0 - dx * 1
         bz = tfma(-ri.dy, T(0), ri.dx * T(0));            // dx * 0 - dy * 0
     } else if constexpr (GEO == kGeoXZ) {
@@ -845,7 +859,7 @@ RTPB_HD void tangent_basis(const Ray<T>& ri, T Nx, T Ny, T Nz, T& cx, T& cy, T& 
     unit_or_zero(bx, by, bz, g);
     if constexpr (GEO == kGeoAxial) {
         cx = tfma(bz, T(0), -by);                         // 0 * bz - 1 * by
-        cy = tfma(-bz, T(0), bx);                         // 1 * bx - 0 * bz
+        cy = tfma(-bz, zero_s(), bx);                     // 1 * bx - 0 * bz
         cz = tfma(-bx, T(0), by * T(0));                  // 0 * by - 0 * bx
     } else if constexpr (GEO == kGeoXZ) {
         cx = tfma(bz, T(0), -(Nz * by));                  // 0 * bz - Nz by
@@ -1002,12 +1016,12 @@ RTPB_HD void lens_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, cons
     const T dn = axdot<GEO>(rf.dx, rf.dy, rf.dz, nx, ny, nz);
     T spx, spy, spz;
     if constexpr (GEO == kGeoAxial) {
-        spx = tfma(-dn, T(0), rf.dx);                 // dx - dn * 0
-        spy = tfma(-dn, T(0), rf.dy);
+        spx = tfma(-dn, zero_s(), rf.dx);             // dx - dn * 0
+        spy = tfma(-dn, zero_s(), rf.dy);
         spz = rf.dz - dn;                             // dz - dn * 1
     } else if constexpr (GEO == kGeoXZ) {
         spx = rf.dx - dn * nx;
-        spy = tfma(-dn, T(0), rf.dy);                 // dy - dn * 0
+        spy = tfma(-dn, zero_s(), rf.dy);             // dy - dn * 0
         spz = rf.dz - dn * nz;
     } else {
         spx = rf.dx - dn * nx; spy = rf.dy - dn * ny; spz = rf.dz - dn * nz;
@@ -1106,8 +1120,9 @@ RTPB_HD bool front_side_fails(const Ray<T>& r, const DevSurface<T>& s) {
 
 // The intersection and the surface normal there (RefractingSurface / ReflectingSurface.propagate RT:1181-1186 with
 // get_intersect / get_normal of FlatSurface RT:1323-1337, PlaneMirror RT:1398-1403, SphericalSurface RT:1467-1516)
-// fwd (positions-only steps): the kAxial sphere's forward-root flag (sphere_root<true>) for the row's final kill; left
-// as it is for other surfaces
+// fwd (positions-only steps): for a kAxial sphere the forward-root flag (sphere_root<true>), for a flat whether the
+// plane lies ahead (t >= 0 or NaN; the row is then not killed here), both for the row's final kill; other spheres
+// leave it as it is
 template <typename T, int KIND, int GEO, class G>
 RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const Rcp<T>& iwl, G* g, T* rxy, Ray<T>& ri,
                             T& Nx, T& Ny, T& Nz, bool* fwd = nullptr) {
@@ -1139,8 +1154,17 @@ RTPB_HD void hit_and_normal(const DevSurface<T>& s, const Ray<T>& r, T n1, const
         }
     } else {                                                           // FLAT, PLANE_MIRROR
         Nx = s.nrm[0]; Ny = s.nrm[1]; Nz = s.nrm[2];
-        ri = to_plane<GEO, GEO>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
-                                static_cast<const Rcp<T>*>(nullptr), g);        // RT:1331-1337, 1398-1403
+        if (fwd) {
+            // positions-only steps: the backward-propagation exclusion reported (*fwd = t >= 0 or NaN) instead of
+            // applied -- the caller folds it into the row's final kill (the sweep's flats: 5-7 VALU fewer per ray)
+            T t;
+            ri = to_plane<GEO, GEO>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, false, iwl, &t,
+                                    static_cast<const Rcp<T>*>(nullptr), g);    // RT:1331-1337, 1398-1403
+            *fwd = !(t < T(0));
+        } else {
+            ri = to_plane<GEO, GEO>(r, Nx, Ny, Nz, s.c[0], s.c[1], s.c[2], n1, true, iwl, static_cast<T*>(nullptr),
+                                    static_cast<const Rcp<T>*>(nullptr), g);
+        }
     }
 }
 
@@ -1177,6 +1201,9 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         T Nx, Ny, Nz;
         Ray<T> ri;
         bool fwd = true;
+        // positions only: a flat's backward exclusion joins the row's final kill (fwd), as a kAxial sphere's root
+        // test does; the history steps apply it to the intersection inside to_plane (there the kill's condition is
+        // the sign test the phase needs anyway: measured 2 VALU cheaper than a separate flag)
         hit_and_normal<T, KIND, GEO>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz, (MODE & kPosOnly) != 0 ? &fwd : nullptr);
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
