@@ -4,17 +4,23 @@ The reference's lightsheet sweep (scripts/2024_04_01_lightsheet.py:53-60, 134-13
 per configuration in a zarr array ``rays`` of shape (n_config, planes, n_rays, 8) chunked one
 configuration per chunk, with ``array_columns`` = x, y, z, dx, dy, dz, phase, wavelength.  zarr is
 not a dependency here, so :class:`HistoryWriter` writes that exact layout as a zarr-v2 directory store
-itself (uncompressed chunks, ``.zarray`` / ``.zattrs`` / ``.zgroup`` JSON), readable by zarr when it is
-installed and by :func:`read_array` otherwise.
+itself (``.zarray`` / ``.zattrs`` / ``.zgroup`` JSON), readable by zarr when it is installed and by
+:func:`read_array` otherwise.  Chunks are stored raw (``compressor: null``) or compressed with zlib (zarr's
+``numcodecs.Zlib``: ``{"id": "zlib", "level": L}``, each chunk one ``zlib.compress`` stream); a configuration may be
+split along the ray axis (``chunk_rays``) so its chunks compress on several threads.  The script's own store uses
+zarr's default Blosc/LZ4 compressor, which needs the c-blosc library (not installed here): the compressed variant
+is a different, zarr-readable codec, and its parity is pinned only by this module's round trips.
 
 Histories may be NumPy arrays or torch CUDA tensors.  Device histories are copied into pinned host
 buffers on a side stream and written by a background thread, so the GPU can trace the next
 configuration while the previous one goes to disk (double-buffered).
 """
+import concurrent.futures
 import json
 import os
 import queue
 import threading
+import zlib
 
 import numpy as np
 
@@ -23,10 +29,37 @@ from . import _engine as E
 ARRAY_COLUMNS = ["x", "y", "z", "dx", "dy", "dz", "phase", "wavelength"]
 
 
-def _zarray(shape, chunks, dtype):
+def _zarray(shape, chunks, dtype, compressor=None):
     return {"zarr_format": 2, "shape": list(shape), "chunks": list(chunks), "dtype": np.dtype(dtype).str,
-            "compressor": None, "fill_value": "NaN" if np.dtype(dtype).kind == "f" else 0, "filters": None,
+            "compressor": compressor, "fill_value": "NaN" if np.dtype(dtype).kind == "f" else 0, "filters": None,
             "order": "C", "dimension_separator": "."}
+
+
+def _codec(compressor):
+    """The zarr compressor metadata for `compressor`: None (raw chunks), "zlib" (level 1), ("zlib", level) or a
+    numcodecs-style dict {"id": "zlib", "level": level}."""
+    if compressor is None:
+        return None
+    if isinstance(compressor, str):
+        compressor = (compressor, 1)
+    if isinstance(compressor, (tuple, list)):
+        compressor = {"id": compressor[0], "level": int(compressor[1])}
+    compressor = dict(compressor)
+    if compressor.get("id") != "zlib" or not 0 <= int(compressor.get("level", 1)) <= 9:
+        raise ValueError(f"unsupported compressor {compressor!r} (None or zlib level 0-9)")
+    return {"id": "zlib", "level": int(compressor.get("level", 1))}
+
+
+def _encode(codec, raw):
+    return raw if codec is None else zlib.compress(raw, codec["level"])
+
+
+def _decode(codec, data):
+    if codec is None:
+        return data
+    if codec.get("id") != "zlib":
+        raise ValueError(f"unsupported compressor {codec!r}")
+    return zlib.decompress(data)
 
 
 def _write_json(path, obj):
@@ -37,17 +70,31 @@ def _write_json(path, obj):
 
 
 class HistoryWriter:
-    """zarr-v2 store at ``path`` with array ``rays`` (n_configs, n_planes, n_rays, 8)."""
+    """zarr-v2 store at ``path`` with array ``rays`` (n_configs, n_planes, n_rays, 8).
 
-    def __init__(self, path, n_configs, n_planes, n_rays, dtype="float64", attrs=None, depth=2):
+    compressor: None (raw chunks, the default), "zlib", ("zlib", level) or {"id": "zlib", "level": level}.
+    chunk_rays: rays per chunk (default: all -- one chunk per configuration, the script's chunks=(1, planes,
+    nrays, 8)); the last chunk of a configuration is stored at full chunk size, padded with the fill value (NaN),
+    as zarr stores edge chunks.  workers: threads compressing / writing one configuration's chunks."""
+
+    def __init__(self, path, n_configs, n_planes, n_rays, dtype="float64", attrs=None, depth=2, compressor=None,
+                 chunk_rays=None, workers=None):
         self.path = str(path)
         self.shape = (int(n_configs), int(n_planes), int(n_rays), 8)
         self.dtype = np.dtype(dtype)
+        self.codec = _codec(compressor)
+        self.chunk_rays = int(chunk_rays) if chunk_rays else max(self.shape[2], 1)
+        if self.chunk_rays < 1:
+            raise ValueError("chunk_rays must be positive")
         os.makedirs(os.path.join(self.path, "rays"), exist_ok=True)
         _write_json(os.path.join(self.path, ".zgroup"), {"zarr_format": 2})
         _write_json(os.path.join(self.path, ".zattrs"), dict(attrs or {}))
-        _write_json(os.path.join(self.path, "rays", ".zarray"), _zarray(self.shape, (1,) + self.shape[1:], self.dtype))
+        _write_json(os.path.join(self.path, "rays", ".zarray"),
+                    _zarray(self.shape, (1, self.shape[1], self.chunk_rays, 8), self.dtype, self.codec))
         _write_json(os.path.join(self.path, "rays", ".zattrs"), {"array_columns": ARRAY_COLUMNS})
+        n_chunks = -(-self.shape[2] // self.chunk_rays)
+        self._pool = concurrent.futures.ThreadPoolExecutor(
+            max_workers=max(1, min(int(workers or min(8, os.cpu_count() or 1)), n_chunks)))
         self._q = queue.Queue(maxsize=depth)
         self._free = queue.Queue()
         self._err = None
@@ -56,8 +103,23 @@ class HistoryWriter:
         self._thread.start()
 
     # -------------------------------------------------------------------- chunks
-    def _chunk_file(self, index):
-        return os.path.join(self.path, "rays", f"{index}.0.0.0")
+    def _chunk_file(self, index, j=0):
+        return os.path.join(self.path, "rays", f"{index}.0.{j}.0")
+
+    def _write_chunk(self, index, j, arr):
+        """Chunk j of configuration `index` (rays j*chunk_rays ...), padded to the chunk shape, encoded, written
+        atomically (zlib releases the GIL: the pool's threads compress in parallel)."""
+        c = self.chunk_rays
+        block = arr[:, j * c:(j + 1) * c]
+        if block.shape[1] < c:
+            pad = np.full((block.shape[0], c, 8), np.nan if self.dtype.kind == "f" else 0, dtype=self.dtype)
+            pad[:, :block.shape[1]] = block
+            block = pad
+        data = _encode(self.codec, memoryview(np.ascontiguousarray(block)).cast("B"))
+        tmp = self._chunk_file(index, j) + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, self._chunk_file(index, j))
 
     def _drain(self):
         while True:
@@ -72,10 +134,12 @@ class HistoryWriter:
                 # the copy has finished: drop the last references to the device history, so its memory may be
                 # freed (and reused by the next trace) while this chunk goes to disk
                 del src
-                tmp = self._chunk_file(index) + ".tmp"
-                with open(tmp, "wb") as f:
-                    f.write(memoryview(np.ascontiguousarray(arr)).cast("B"))
-                os.replace(tmp, self._chunk_file(index))
+                n_chunks = -(-self.shape[2] // self.chunk_rays)
+                if n_chunks == 1:
+                    self._write_chunk(index, 0, arr)
+                else:
+                    for f in [self._pool.submit(self._write_chunk, index, j, arr) for j in range(n_chunks)]:
+                        f.result()
             except Exception as e:  # surfaced by the next write()/close()
                 self._err = e
             finally:
@@ -124,6 +188,7 @@ class HistoryWriter:
     def close(self):
         self._q.put(None)
         self._thread.join()
+        self._pool.shutdown()
         if self._err is not None:
             raise self._err
 
@@ -141,13 +206,15 @@ def read_array(path, name="rays"):
     dtype = np.dtype(meta["dtype"])
     shape, chunks = tuple(meta["shape"]), tuple(meta["chunks"])
     fill = np.nan if meta["fill_value"] == "NaN" else meta["fill_value"]
+    codec = meta.get("compressor")
     out = np.full(shape, fill, dtype=dtype)
     grid = [range(-(-s // c)) for s, c in zip(shape, chunks)]
     for idx in np.ndindex(*[len(g) for g in grid]):
         fn = os.path.join(path, name, ".".join(str(i) for i in idx) if idx else "0")
         if not os.path.exists(fn):
             continue
-        block = np.fromfile(fn, dtype=dtype).reshape(chunks)
+        with open(fn, "rb") as f:
+            block = np.frombuffer(_decode(codec, f.read()), dtype=dtype).reshape(chunks)
         sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(idx, chunks, shape))
         out[sl] = block[tuple(slice(0, x.stop - x.start) for x in sl)]
     return out
