@@ -75,7 +75,8 @@ class HistoryWriter:
     compressor: None (raw chunks, the default), "zlib", ("zlib", level) or {"id": "zlib", "level": level}.
     chunk_rays: rays per chunk (default: all -- one chunk per configuration, the script's chunks=(1, planes,
     nrays, 8)); the last chunk of a configuration is stored at full chunk size, padded with the fill value (NaN),
-    as zarr stores edge chunks.  workers: threads compressing / writing one configuration's chunks."""
+    as zarr stores edge chunks.  workers: threads encoding and writing chunks; compressed configurations with fewer
+    chunks than workers are encoded up to ``depth`` at a time (raw ones one at a time)."""
 
     def __init__(self, path, n_configs, n_planes, n_rays, dtype="float64", attrs=None, depth=2, compressor=None,
                  chunk_rays=None, workers=None):
@@ -92,9 +93,14 @@ class HistoryWriter:
         _write_json(os.path.join(self.path, "rays", ".zarray"),
                     _zarray(self.shape, (1, self.shape[1], self.chunk_rays, 8), self.dtype, self.codec))
         _write_json(os.path.join(self.path, "rays", ".zattrs"), {"array_columns": ARRAY_COLUMNS})
-        n_chunks = -(-self.shape[2] // self.chunk_rays)
-        self._pool = concurrent.futures.ThreadPoolExecutor(
-            max_workers=max(1, min(int(workers or min(8, os.cpu_count() or 1)), n_chunks)))
+        self._n_chunks = -(-self.shape[2] // self.chunk_rays)
+        n_workers = max(1, int(workers or min(8, os.cpu_count() or 1)))
+        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=n_workers)
+        # configurations whose chunks are encoded at once (each holds its host copy until written): raw chunks one
+        # at a time, as the disk takes them; compressed ones up to `depth`, enough to keep the workers busy when a
+        # configuration has fewer chunks than there are workers
+        inflight = 1 if self.codec is None else max(1, min(int(depth), -(-n_workers // max(self._n_chunks, 1))))
+        self._inflight = threading.BoundedSemaphore(inflight)
         self._q = queue.Queue(maxsize=depth)
         self._free = queue.Queue()
         self._err = None
@@ -134,17 +140,33 @@ class HistoryWriter:
                 # the copy has finished: drop the last references to the device history, so its memory may be
                 # freed (and reused by the next trace) while this chunk goes to disk
                 del src
-                n_chunks = -(-self.shape[2] // self.chunk_rays)
-                if n_chunks == 1:
-                    self._write_chunk(index, 0, arr)
-                else:
-                    for f in [self._pool.submit(self._write_chunk, index, j, arr) for j in range(n_chunks)]:
-                        f.result()
             except Exception as e:  # surfaced by the next write()/close()
                 self._err = e
-            finally:
                 if buf is not None:
                     self._free.put(buf)
+                continue
+            if self._n_chunks == 0:
+                if buf is not None:
+                    self._free.put(buf)
+                continue
+            # the configuration's chunks go to the pool; its host copy returns to the free list when the last one
+            # is written, and the semaphore bounds the configurations in flight (and so the host copies held)
+            self._inflight.acquire()
+            left = [self._n_chunks]
+            lock = threading.Lock()
+
+            def done(fut, buf=buf):
+                if fut.exception() is not None:
+                    self._err = fut.exception()
+                with lock:
+                    left[0] -= 1
+                    last = left[0] == 0
+                if last:
+                    if buf is not None:
+                        self._free.put(buf)
+                    self._inflight.release()
+            for j in range(self._n_chunks):
+                self._pool.submit(self._write_chunk, index, j, arr).add_done_callback(done)
 
     def write(self, index, history):
         """Store ``history`` (n_planes, n_rays, 8) as configuration ``index`` (asynchronous)."""
@@ -188,7 +210,7 @@ class HistoryWriter:
     def close(self):
         self._q.put(None)
         self._thread.join()
-        self._pool.shutdown()
+        self._pool.shutdown(wait=True)
         if self._err is not None:
             raise self._err
 
