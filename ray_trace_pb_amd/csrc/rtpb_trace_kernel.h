@@ -150,13 +150,21 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     };
     if constexpr (kFinal) {
         T n_cur = mat_n(mats);
-        for (int s = 0; s < a.nsurf; ++s) {
-            const T n_next = mat_n(mats + s + 1);
-            Ray<T> after;
-            propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_next, iwl,
-                                             [](const Ray<T>&) {}, after);
-            r = after;
-            n_cur = n_next;
+        // two surfaces per iteration, the second writing straight into the loop-carried ray: the register
+        // allocator cannot coalesce a step's output with the ray it read across the kind switch (a copy of all
+        // eight values per surface otherwise)
+        for (int s = 0; s < a.nsurf; s += 2) {
+            const T n_mid = mat_n(mats + s + 1);
+            Ray<T> mid;
+            propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_mid, iwl, [](const Ray<T>&) {}, mid);
+            if (s + 1 < a.nsurf) {
+                const T n_next = mat_n(mats + s + 2);
+                propagate_surface_emit<T, kLens>(surface(s + 1), mid, n_mid, n_next, iwl, [](const Ray<T>&) {}, r);
+                n_cur = n_next;
+            } else {
+                r = mid;
+                n_cur = n_mid;
+            }
         }
         if constexpr (kXchg) {
             xchg_flush<kNT>(out, ray0, a.n, lane, r);
@@ -182,8 +190,9 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         }
         slot_off += a.out_ps;
     }
-    T n_cur = mat_n(mats);
-    for (int s = 0; s < a.nsurf; ++s) {
+    // one surface with its planes: `in` -> `out` (two per iteration below, so the second writes straight into the
+    // loop-carried ray -- no per-surface copy of the ray across the kind switch)
+    auto one = [&](int s, const Ray<T>& in, T n_in, Ray<T>& res, T& n_res) {
         const T n_next = mat_n(mats + s + 1);
         const int p = 2 * s + 1;
         const bool st_at = plane_bit(a.mask_lo, a.mask_hi, p);          // wave-uniform
@@ -202,21 +211,31 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
                 if (valid && st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
             }
         };
-        Ray<T> after;
-        propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_next, iwl, emit_at, after);
+        propagate_surface_emit<T, kLens>(surface(s), in, n_in, n_next, iwl, emit_at, res);
         if constexpr (kXchg) {
-            if (st_after) xchg_flush<kNT>(out + off_after, ray0, a.n, lane, after);
+            if (st_after) xchg_flush<kNT>(out + off_after, ray0, a.n, lane, res);
         } else if constexpr (kStaged) {
             // both planes of the surface share one LDS round trip
-            if (st_after) tile_write<TS>(tile_b, lane, after);
+            if (st_after) tile_write<TS>(tile_b, lane, res);
             if (st_at || st_after) lds_wait();
             if (st_at) tile_flush<TS, kNT>(tile_a, out + off_at, ray0, a.n, lane);
             if (st_after) tile_flush<TS, kNT>(tile_b, out + off_after, ray0, a.n, lane);
         } else if (valid) {
-            if (st_after) store_ray<TS, OUT_LAYOUT>(out + off_after, i, a.out_fs, after);
+            if (st_after) store_ray<TS, OUT_LAYOUT>(out + off_after, i, a.out_fs, res);
         }
-        r = after;
-        n_cur = n_next;
+        n_res = n_next;
+    };
+    T n_cur = mat_n(mats);
+    for (int s = 0; s < a.nsurf; s += 2) {
+        Ray<T> mid;
+        T n_mid;
+        one(s, r, n_cur, mid, n_mid);
+        if (s + 1 < a.nsurf) {
+            one(s + 1, mid, n_mid, r, n_cur);
+        } else {
+            r = mid;
+            n_cur = n_mid;
+        }
     }
     };
     body(static_cast<int64_t>(blockIdx.x));

@@ -12,7 +12,8 @@ where they come from without a GPU.
 --kernel compiles the shipped history kernel (trace_kernel, the C4 variant: float64 input, float32 AOS history,
 LDS-staged non-temporal stores, PerfectLens code) from a scratch copy of csrc/ whose dispatch_kind always takes one
 (kind, geometry form), and counts the VALU of one surface-loop iteration on the fast path -- the per-surface cost
-tools/history_kind_cost.py measures with PMC, without a GPU.
+tools/history_kind_cost.py measures with PMC, without a GPU (the kernel's loop runs two surfaces per iteration, so
+--kernel reports half an iteration).
 """
 import argparse
 import collections
@@ -269,9 +270,10 @@ def kernel_main(show, final=False):
         (gname, gbody), = g_funcs.items()
         guarded = [x for x in guarded_walk(loop_blocks(gbody, 1), header_of(gbody, 1)) if not x.startswith("v_cvt")]
         on = [x for x in on if not x.startswith("v_cvt")]
-        print(f"{case:11s} surface-loop VALU (+{0 if final else 16} cvt) {len(on):4d} fast path, {len(guarded):4d} "
-              f"with the guards  "
-              f"(f64 arithmetic {f64:3d}, moves {movs:3d}, loop blocks {len(blks)})", flush=True)
+        # the surface loop runs two surfaces per iteration (rtpb_trace_kernel.h): per surface = half
+        print(f"{case:11s} per surface VALU (+{0 if final else 16} cvt) {len(on) / 2:6.1f} fast path, "
+              f"{len(guarded) / 2:6.1f} with the guards  (f64 arithmetic {f64 / 2:5.1f}, moves {movs / 2:4.1f}, "
+              f"loop blocks {len(blks)})", flush=True)
         if show == case + "+g":
             for x in guarded:
                 print("    " + x)
