@@ -5,6 +5,7 @@ prefixes give the cost of one lens step and one flat step per ray; the 12-sphere
 per-ray generation, first-surface sharing and reduction spread over them).
 
     python tools/c5_kind_cost.py --run OUT          # the three PMC runs, then the table
+    python tools/c5_kind_cost.py --run OUT --ks 1 2 3 12 13 14   # + the fixed per-ray part (K = 1, 2, 3 surfaces)
     python tools/c5_kind_cost.py --surfaces 13      # one sweep (what each PMC run executes)
 """
 import argparse
@@ -35,10 +36,10 @@ def sweep(k):
           f"count {int(summ['count'].sum())}", flush=True)
 
 
-def run(out):
+def run(out, ks=(12, 13, 14)):
     env = dict(os.environ, TMPDIR="/tmp")
     res = {}
-    for k in (12, 13, 14):
+    for k in ks:
         d = os.path.join(out, f"k{k}")
         cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--pmc", "SQ_INSTS_VALU", "--output-format", "csv", "-d", d,
                "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--surfaces", str(k)]
@@ -55,18 +56,29 @@ def run(out):
         res[k] = tot
     rays = 7 * 3163 * 3162
     per_ray = {k: v * 64 / rays for k, v in res.items()}    # wave-instructions -> per ray (64 lanes)
-    print(f"VALU per ray: 12 surfaces {per_ray[12]:.1f} ({per_ray[12] / 12:.1f} per sphere incl. generation, sharing "
-          f"and reduction), lens step {per_ray[13] - per_ray[12]:.1f}, flat step {per_ray[14] - per_ray[13]:.1f}, "
-          f"whole system {per_ray[14]:.1f} = {per_ray[14] / 14:.1f} per ray-surface")
+    for k in sorted(per_ray):
+        print(f"surfaces {k:2d}: {per_ray[k]:8.1f} VALU per ray", flush=True)
+    if all(k in per_ray for k in (1, 2, 3)):
+        # K = 1: generation, the shared first sphere and the reduction; K = 2, 3 add one and two sphere steps
+        step = (per_ray[3] - per_ray[1]) / 2
+        print(f"fixed per-ray part (generation, first surface shared over the bundle, reduction, run switches): "
+              f"{per_ray[1]:.1f} = K=1; a sphere step {step:.1f}; fixed part beyond one step {per_ray[1] - step:.1f}")
+    if all(k in per_ray for k in (12, 13, 14)):
+        print(f"VALU per ray: 12 surfaces {per_ray[12]:.1f} ({per_ray[12] / 12:.1f} per sphere incl. generation, "
+              f"sharing and reduction), lens step {per_ray[13] - per_ray[12]:.1f}, flat step "
+              f"{per_ray[14] - per_ray[13]:.1f}, whole system {per_ray[14]:.1f} = {per_ray[14] / 14:.1f} per "
+              f"ray-surface")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--run", default="")
     ap.add_argument("--surfaces", type=int, default=14)
+    ap.add_argument("--ks", type=int, nargs="+", default=[12, 13, 14],
+                    help="--run: the prefixes (numbers of surfaces) to count")
     a = ap.parse_args()
     if a.run:
-        run(a.run)
+        run(a.run, tuple(a.ks))
     else:
         sweep(a.surfaces)
 
