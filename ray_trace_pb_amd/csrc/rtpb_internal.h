@@ -84,14 +84,27 @@ struct TraceArgs {
 };
 
 // The trace kernel's launcher for one (input, storage) type pair: picks the kernel variant for the
-// layouts, the tuning knobs and the plan's features (rtpb_trace_kernel.h; instantiated in
-// rtpb_trace_<tin>_<ts>.hip).
+// layouts, the tuning knobs and the plan's features (rtpb_trace_kernel.h).  The plan-feature variants come in two
+// groups compiled in separate translation units (rtpb_trace_<tin>_<ts>.hip: group 0, ..._g1.hip: group 1), so the
+// eight largest compiles of the library run in parallel.
+// group 0: feat 0, 1, 4, 5 (constant / Sellmeier / LDS-table media, with or without PerfectLens code);
+// group 1: feat 16, 17 (indexed materials) and 15 (everything)
+constexpr int trace_feat_group(int feat) { return (feat == 0 || feat == 1 || feat == 4 || feat == 5) ? 0 : 1; }
+template <typename TIN, typename TS, int GROUP>
+hipError_t launch_trace_group(const TraceArgs<TIN, TS>& a, int il, int ol, int feat, hipStream_t st);
+#define RTPB_TRACE_GROUP_EXTERN(TI, TS)                                                                             \
+    extern template hipError_t launch_trace_group<TI, TS, 0>(const TraceArgs<TI, TS>&, int, int, int, hipStream_t); \
+    extern template hipError_t launch_trace_group<TI, TS, 1>(const TraceArgs<TI, TS>&, int, int, int, hipStream_t);
+RTPB_TRACE_GROUP_EXTERN(double, double)
+RTPB_TRACE_GROUP_EXTERN(float, float)
+RTPB_TRACE_GROUP_EXTERN(double, float)
+RTPB_TRACE_GROUP_EXTERN(float, double)
+#undef RTPB_TRACE_GROUP_EXTERN
 template <typename TIN, typename TS>
-hipError_t launch_trace(const TraceArgs<TIN, TS>& a, int il, int ol, int feat, hipStream_t st);
-extern template hipError_t launch_trace<double, double>(const TraceArgs<double, double>&, int, int, int, hipStream_t);
-extern template hipError_t launch_trace<float, float>(const TraceArgs<float, float>&, int, int, int, hipStream_t);
-extern template hipError_t launch_trace<double, float>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
-extern template hipError_t launch_trace<float, double>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
+inline hipError_t launch_trace(const TraceArgs<TIN, TS>& a, int il, int ol, int feat, hipStream_t st) {
+    return trace_feat_group(feat) == 0 ? launch_trace_group<TIN, TS, 0>(a, il, ol, feat, st)
+                                       : launch_trace_group<TIN, TS, 1>(a, il, ol, feat, st);
+}
 // tuning knobs (rtpb_set_tuning, defined in rtpb_trace.hip)
 extern std::atomic<int> g_aos_staging, g_nt_stores, g_stage_input, g_host_chunk_mib, g_indexed_materials;
 int set_buffer_pool_keep(int64_t k);              // rtpb_buffers.hip: rtpb_set_tuning("buffer_pool_buffers")

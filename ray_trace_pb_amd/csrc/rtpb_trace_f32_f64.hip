@@ -1,6 +1,6 @@
-// Trace kernel variants for f32 input rays and f64 history storage (see rtpb_trace_kernel.h).
+// Trace kernel variants for f32 input rays and f64 history storage, plan-feature group 0 (feat 0, 1, 4, 5) (see rtpb_trace_kernel.h).
 #include "rtpb_trace_kernel.h"
 
 namespace rtpbi {
-template hipError_t launch_trace<float, double>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
+template hipError_t launch_trace_group<float, double, 0>(const TraceArgs<float, double>&, int, int, int, hipStream_t);
 }  // namespace rtpbi

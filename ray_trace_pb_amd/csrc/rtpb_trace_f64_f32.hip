@@ -1,6 +1,6 @@
-// Trace kernel variants for f64 input rays and f32 history storage (see rtpb_trace_kernel.h).
+// Trace kernel variants for f64 input rays and f32 history storage, plan-feature group 0 (feat 0, 1, 4, 5) (see rtpb_trace_kernel.h).
 #include "rtpb_trace_kernel.h"
 
 namespace rtpbi {
-template hipError_t launch_trace<double, float>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
+template hipError_t launch_trace_group<double, float, 0>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
 }  // namespace rtpbi

@@ -1,0 +1,6 @@
+// Trace kernel variants for f64 input rays and f32 history storage, plan-feature group 1 (feat 15, 16, 17) (see rtpb_trace_kernel.h).
+#include "rtpb_trace_kernel.h"
+
+namespace rtpbi {
+template hipError_t launch_trace_group<double, float, 1>(const TraceArgs<double, float>&, int, int, int, hipStream_t);
+}  // namespace rtpbi

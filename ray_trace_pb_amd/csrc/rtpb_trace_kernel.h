@@ -1,7 +1,7 @@
 // rtpb_trace_kernel.h -- the fused trace kernel (the hot path) and its launch dispatch, templated on
-// the input element type TIN and the storage type TS.  Each rtpb_trace_<tin>_<ts>.hip translation unit
-// instantiates launch_trace for one (TIN, TS) pair so the variants compile in parallel; the host side
-// (rtpb_trace.hip) only sees the declaration in rtpb_internal.h.
+// the input element type TIN and the storage type TS.  Each rtpb_trace_<tin>_<ts>[_g1].hip translation unit
+// instantiates launch_trace_group for one (TIN, TS) pair and one group of plan-feature variants, so the variants
+// compile in parallel; the host side (rtpb_trace.hip) only sees launch_trace in rtpb_internal.h.
 //
 // plan (replacing System.ray_trace's surface loop RT:658-659 and the per-surface NumPy ufunc chains of
 // RT:1160-1801), plus the host-buffer pipeline, tuning knobs and launch timing of the C ABI.
@@ -254,27 +254,33 @@ hipError_t launch_w(const TraceArgs<TI, T>& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <typename TI, typename T, int IL, int OL, int ST>
+template <typename TI, typename T, int IL, int OL, int ST, int GROUP>
 hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
     // float64 final-plane-only kernels (compute-bound: the C5 / focus-finding mode) are held to >= 6
     // waves per SIMD (<= 80 VGPRs, no spill; 7 and 8 measured slower); everything else keeps the
     // compiler's choice (the history kernels are bound by their LDS tiles and store stream: 6-8 waves
     // measured no faster; the float32 final-only variants would spill)
 #define RTPB_WPE(F) (((ST & 8) && sizeof(T) == 8 && (F) != 15) ? 6 : 1)
-    switch (feat) {
-    case 0: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(0), 0>(a, st);
-    case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
-    case 4: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(4), 4>(a, st);
-    case 5: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(5), 5>(a, st);
-    case 16: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(16), 16>(a, st);
-    case 17: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(17), 17>(a, st);
-    default: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(15), 15>(a, st);   // POLY6 or a large table: everything in
+    if constexpr (GROUP == 0) {
+        switch (feat) {
+        case 0: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(0), 0>(a, st);
+        case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
+        case 4: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(4), 4>(a, st);
+        case 5: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(5), 5>(a, st);
+        default: return hipErrorInvalidValue;                                // another group's feature set
+        }
+    } else {
+        switch (feat) {
+        case 16: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(16), 16>(a, st);
+        case 17: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(17), 17>(a, st);
+        default: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(15), 15>(a, st);   // POLY6 or a large table: everything
+        }
     }
 #undef RTPB_WPE
 }
 
-template <typename TI, typename T>
-hipError_t launch_trace(const TraceArgs<TI, T>& a, int il, int ol, int feat, hipStream_t st) {
+template <typename TI, typename T, int G>
+hipError_t launch_trace_group(const TraceArgs<TI, T>& a, int il, int ol, int feat, hipStream_t st) {
     const int staging = g_aos_staging.load();
     const bool staged = staging != 0;
     const bool nt = g_nt_stores.load() != 0;
@@ -287,32 +293,32 @@ hipError_t launch_trace(const TraceArgs<TI, T>& a, int il, int ol, int feat, hip
     if (final_only && ol == RTPB_AOS && il == RTPB_AOS && staged && nt && !g_stage_input.load())
     {
         if constexpr (kF32) {
-            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 27>(a, feat, st);
+            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 27, G>(a, feat, st);
         }
-        return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 11>(a, feat, st);
+        return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 11, G>(a, feat, st);
     }
     if constexpr (!std::is_same<TI, T>::value) {
         // input and storage types differ: AOS input only (rtpb_trace checks), no staged-input variant
-        if (ol == RTPB_SOA) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
-        if (!staged) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st);
+        if (ol == RTPB_SOA) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0, G>(a, feat, st);
+        if (!staged) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0, G>(a, feat, st);
         if constexpr (kF32) {
-            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19>(a, feat, st);
+            if (xchg) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19, G>(a, feat, st);
         }
-        return nt ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st);
+        return nt ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3, G>(a, feat, st) : launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1, G>(a, feat, st);
     }
     if (ol == RTPB_AOS) {
         if (!staged)
-            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 0>(a, feat, st);
-        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 7>(a, feat, st);
+            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 0, G>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 0, G>(a, feat, st);
+        if (nt && il == RTPB_AOS && g_stage_input.load()) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 7, G>(a, feat, st);
         if constexpr (kF32) {
-            if (xchg && il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19>(a, feat, st);
+            if (xchg && il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_AOS, 19, G>(a, feat, st);
         }
         if (nt)
-            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 3>(a, feat, st);
-        return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 1>(a, feat, st);
+            return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 3, G>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 3, G>(a, feat, st);
+        return il == RTPB_AOS ? launch_one<TI, T, RTPB_AOS, RTPB_AOS, 1, G>(a, feat, st) : launch_one<TI, T, RTPB_SOA, RTPB_AOS, 1, G>(a, feat, st);
     }
-    if (il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0>(a, feat, st);
-    return launch_one<TI, T, RTPB_SOA, RTPB_SOA, 0>(a, feat, st);
+    if (il == RTPB_AOS) return launch_one<TI, T, RTPB_AOS, RTPB_SOA, 0, G>(a, feat, st);
+    return launch_one<TI, T, RTPB_SOA, RTPB_SOA, 0, G>(a, feat, st);
 }
 
 

@@ -46,7 +46,7 @@ def _findings(path):
 def test_no_undef_copy_kills_in_device_code(tmp_path):
     srcs = sorted(glob.glob(os.path.join(_build.CSRC, "*.hip")))
     assert srcs
-    workers = max(1, min(len(srcs), (os.cpu_count() or 2) // 2, 4))
+    workers = max(1, min(len(srcs), os.cpu_count() or 2, 8))
     with concurrent.futures.ThreadPoolExecutor(workers) as ex:
         outs = list(ex.map(lambda s: _asm(s, str(tmp_path)), srcs))
     bad = [f for o in outs for f in _findings(o)]
