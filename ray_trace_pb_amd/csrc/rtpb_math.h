@@ -118,11 +118,12 @@ __device__ __forceinline__ int class_mask(int k) {
 
 // Guard policies of the exact fast paths below.  Each shortcut is exact only inside a range of its
 // operands; outside it the operation must take the compiler's full sequence.
-//   GuardBranch: a per-operation branch to the full sequence (default; the all-planes history kernels).
-//   GuardDefer:  no branch -- the operation only records that a lane left the range (g->bad); the caller
-//                re-traces such rays with GuardBranch afterwards.  Removing the per-operation branches
-//                lets the compiler schedule a whole surface as one block (final-plane kernels and the
-//                spot sweep: -20 % and more).
+//   GuardBranch: a per-operation branch to the full sequence -- what every shipped kernel uses.
+//   GuardDefer:  no branch -- the operation only records that a lane left the range (g->bad) and a caller would
+//                re-trace such rays with GuardBranch.  Measured slower in every kernel (DESIGN.md §5, round 3:
+//                the re-trace path raises register use, and the flags cost more VALU than the branches' exec
+//                updates); kept for tests/native/fastdiv_check.hip, which checks that the flags are raised
+//                exactly where a shortcut leaves its exact range (tests/test_gpu_fastdiv.py).
 struct GuardBranch { static constexpr bool kDefer = false; };
 struct GuardDefer { static constexpr bool kDefer = true; bool bad = false; };
 

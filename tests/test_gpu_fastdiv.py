@@ -119,7 +119,8 @@ def test_fastdiv_specials():
 
 def test_deferred_guards_flag_only_out_of_range_operands():
     """Ordinary operands (the magnitudes a trace produces, zeros and infinities included) are never
-    flagged by the GuardDefer forms: the final-plane kernels re-trace only pathological rays."""
+    flagged by the GuardDefer forms (the shortcuts' exact ranges cover them: a deferred-guard kernel would re-trace
+    only pathological rays)."""
     rng = np.random.default_rng(11)
     n = 200_000
     a = _pow2_band(rng, n, -300, 300)
