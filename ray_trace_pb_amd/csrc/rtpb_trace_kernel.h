@@ -46,8 +46,8 @@ constexpr int trace_block(int out_layout, int store) {
 // stores for the staged tiles, bit 2 = LDS-staged AOS input loads, bit 3 = final plane only.
 // FEAT: bit 0 = PerfectLens code, bit 1 = RTPB_POLY6 code compiled in, bit 2 = TABLE materials looked up
 // in an LDS copy of the plan's table (dynamic LDS, copied at launch), bit 3 = TABLE materials looked up
-// in global memory.  Leaving out what a plan does not use lowers register pressure (f64 staged: 92 VGPRs
-// without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
+// in global memory.  Leaving out what a plan does not use lowers register pressure (round 2's f64 staged kernels:
+// 92 VGPRs without the PerfectLens code, 100 with both), 10-15 % faster when compute-bound, and without a global
 // table lookup the surface loop never waits on the vmcnt counter, which on gfx950 would also wait for
 // every history store in flight (see kLdsTablePairs).  rtpb_plan::feat picks the variant.
 template <typename TIN, typename TS, int IN_LAYOUT, int OUT_LAYOUT, int STORE, int WPE, int FEAT>
