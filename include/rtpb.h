@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define RTPB_ABI_VERSION 8   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
+#define RTPB_ABI_VERSION 9   /* 2: + *_tables generators, surface-hook kernels, sorted-table lookup
                                 3: input element type separate from the storage type (in_dtype)
                                 4: + rtpb_trace_checked (table-miss flag)
                                 5: + rtpb_buffer_alloc / _free / _dlpack (placement-robust history buffers)
@@ -52,7 +52,8 @@ extern "C" {
                                 8: + rtpb_trace_f64 / rtpb_trace_f32 (one-shot calls),
                                    rtpb_oneshot_plans / rtpb_oneshot_clear; freeing a library buffer
                                    never synchronises the device (retired mappings are released by the
-                                   next allocation that maps new memory, or by rtpb_buffer_trim) */
+                                   next allocation that maps new memory, or by rtpb_buffer_trim)
+                                9: + rtpb_trace_packed (rtpb_trace_checked's arguments in one struct) */
 
 /* ---- error codes ---------------------------------------------------------------------------- */
 #define RTPB_OK 0
@@ -217,6 +218,28 @@ int rtpb_trace_checked(const rtpb_plan* plan, int32_t device,
                        int64_t in_field_stride, void* out, int32_t out_layout, int64_t out_plane_stride,
                        int64_t out_field_stride, uint64_t plane_mask_lo, uint64_t plane_mask_hi, void* stream,
                        int32_t* table_miss);
+
+/* rtpb_trace_checked with its arguments in one struct (same fields, same meaning; table_miss may be NULL).  For
+   bindings whose per-argument marshalling costs more than the call (ctypes: ~0.2 us per argument): the caller keeps
+   a filled struct per (plan, shape, planes, stream) and updates the buffer pointers between calls. */
+typedef struct rtpb_trace_call {
+    const rtpb_plan* plan;
+    const void* rays_in;
+    void* out;
+    void* stream;
+    int32_t* table_miss;
+    int64_t n_rays;
+    int64_t in_field_stride;
+    int64_t out_plane_stride;
+    int64_t out_field_stride;
+    uint64_t plane_mask_lo;
+    uint64_t plane_mask_hi;
+    int32_t device;
+    int32_t in_dtype;
+    int32_t in_layout;
+    int32_t out_layout;
+} rtpb_trace_call;
+int rtpb_trace_packed(const rtpb_trace_call* call);
 
 /* ---- one-shot calls (the replacement of RT:658-659 without a plan handle) ------- */
 /* The whole system in one call: `surfaces` (nsurf) and `materials` (nmat = nsurf + 1: initial material,

@@ -11,7 +11,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librtpb.so")
 
-RTPB_ABI_VERSION = 8
+RTPB_ABI_VERSION = 9
 RTPB_F64, RTPB_F32 = 0, 1
 RTPB_AOS, RTPB_SOA = 0, 1
 RTPB_REFRACT, RTPB_REFLECT = 0, 1
@@ -46,6 +46,16 @@ class Material(ctypes.Structure):
                 ("table", ctypes.POINTER(ctypes.c_double))]
 
 
+class TraceCall(ctypes.Structure):
+    """struct rtpb_trace_call (rtpb_trace_packed)"""
+    _fields_ = [("plan", ctypes.c_void_p), ("rays_in", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("stream", ctypes.c_void_p), ("table_miss", ctypes.c_void_p), ("n_rays", ctypes.c_int64),
+                ("in_field_stride", ctypes.c_int64), ("out_plane_stride", ctypes.c_int64),
+                ("out_field_stride", ctypes.c_int64), ("plane_mask_lo", ctypes.c_uint64),
+                ("plane_mask_hi", ctypes.c_uint64), ("device", ctypes.c_int32), ("in_dtype", ctypes.c_int32),
+                ("in_layout", ctypes.c_int32), ("out_layout", ctypes.c_int32)]
+
+
 # symbol -> (restype, argtypes); every symbol include/rtpb.h declares
 _P = ctypes.c_void_p
 _i32, _i64, _u64, _dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
@@ -68,6 +78,7 @@ SIGNATURES = {
                                         ctypes.POINTER(_P)]),
     "rtpb_plan_destroy": (ctypes.c_int, [_P]),
     "rtpb_trace": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P]),
+    "rtpb_trace_packed": (ctypes.c_int, [ctypes.POINTER(TraceCall)]),
     "rtpb_trace_checked": (ctypes.c_int, [_P, _i32, _P, _i32, _i64, _i32, _i64, _P, _i32, _i64, _i64, _u64, _u64, _P,
                                           _P]),
     "rtpb_trace_f64": (ctypes.c_int, [ctypes.POINTER(Surface), _i32, ctypes.POINTER(Material), _i32, _P, _i64, _P,

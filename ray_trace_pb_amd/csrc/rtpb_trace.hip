@@ -254,6 +254,15 @@ int rtpb_trace(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int
                               out_plane_stride, out_field_stride, plane_mask_lo, plane_mask_hi, stream, nullptr);
 }
 
+static_assert(sizeof(rtpb_trace_call) == 5 * 8 + 6 * 8 + 4 * 4, "rtpb_trace_call: no padding (bindings mirror it)");
+
+int rtpb_trace_packed(const rtpb_trace_call* c) {
+    if (!c) return fail(RTPB_E_INVALID, "call is NULL");
+    return rtpb_trace_checked(c->plan, c->device, c->rays_in, c->in_dtype, c->n_rays, c->in_layout, c->in_field_stride,
+                              c->out, c->out_layout, c->out_plane_stride, c->out_field_stride, c->plane_mask_lo,
+                              c->plane_mask_hi, c->stream, c->table_miss);
+}
+
 int rtpb_trace_checked(const rtpb_plan* plan_c, int32_t device, const void* rays_in, int32_t in_dtype,
                        int64_t n_rays, int32_t in_layout, int64_t in_field_stride, void* out, int32_t out_layout,
                        int64_t out_plane_stride, int64_t out_field_stride, uint64_t plane_mask_lo,

@@ -35,6 +35,21 @@ def test_struct_layouts_match_header():
     # rtpb_surface: 2 x int32 + 9 doubles (3 vectors) + 6 doubles; rtpb_material: 2 x int32 + 6 doubles + ptr
     assert ctypes.sizeof(C.Surface) == 8 + 8 * 15
     assert ctypes.sizeof(C.Material) == 8 + 8 * 6 + 8
+    # rtpb_trace_call: 5 pointers, 4 int64 + 2 uint64, 4 int32 -- field order as in include/rtpb.h
+    assert ctypes.sizeof(C.TraceCall) == 5 * 8 + 6 * 8 + 4 * 4
+    assert [f for f, _ in C.TraceCall._fields_] == [
+        "plan", "rays_in", "out", "stream", "table_miss", "n_rays", "in_field_stride", "out_plane_stride",
+        "out_field_stride", "plane_mask_lo", "plane_mask_hi", "device", "in_dtype", "in_layout", "out_layout"]
+
+
+def test_packed_trace_validates_without_a_gpu():
+    """rtpb_trace_packed: a NULL block and a NULL plan are rejected before any device work."""
+    lib = C.lib()
+    assert lib.rtpb_trace_packed(None) == C.RTPB_E_INVALID
+    assert b"NULL" in lib.rtpb_last_error()
+    c = C.TraceCall(n_rays=4, out_plane_stride=32, out_field_stride=4, plane_mask_lo=1)
+    assert lib.rtpb_trace_packed(ctypes.byref(c)) == C.RTPB_E_INVALID
+    assert b"plan is NULL" in lib.rtpb_last_error()
 
 
 def test_abi_version_and_device_count():
