@@ -757,7 +757,16 @@ def pool_empty(shape, dtype, device, stream=None):
     if pool is None:
         pool = history_pool(idx)
     pid = _POOL_IDS[idx]
-    dev_ctx = torch.cuda.device(idx) if idx != torch.cuda.current_device() else contextlib.nullcontext()
+    on_current = idx == torch.cuda.current_device()
+    if stream is None and on_current:
+        # the drop-in call's case (current device and stream): no context managers
+        _begin_pool(idx, pid)
+        try:
+            return torch.empty(shape, dtype=dtype, device=dev if dev.index is not None else torch.device("cuda", idx))
+        finally:
+            _end_pool(idx, pid)
+            _release_pool(idx, pid)
+    dev_ctx = torch.cuda.device(idx) if not on_current else contextlib.nullcontext()
     with dev_ctx:
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
