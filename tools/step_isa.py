@@ -290,8 +290,9 @@ def guarded_walk(blks, header):
     """VALU of one loop iteration of the shipped code (guards compiled in), from the loop header, when every lane
     stays on the fast paths: an execnz branch (rare lanes' out-of-line code) is not taken; the else side of an if
     (s_andn2_saveexec, execz) runs when its then side went out of line (an execnz just before), else it is skipped;
-    any other forward branch skips code that starts with a full division / square-root sequence or is a NaN fill; a
-    branch back to the header ends the iteration.  Plane stores under uniform branches are not followed (the
+    any other exec-mask branch skips code that starts with a full division / square-root sequence or is a NaN fill;
+    wave-uniform branches (scc / vcc: loop control, plane stores) fall through; a branch back to the header ends the
+    iteration.  Plane stores under uniform branches are not followed (the
     float32 conversions are counted apart)."""
     index = {lab: k for k, (lab, _) in enumerate(blks)}
     k, seen, out = index[header], set(), []
@@ -316,6 +317,8 @@ def guarded_walk(blks, header):
                 break
             if kind.startswith("cbranch_execnz") or t is None or t <= k:
                 continue
+            if kind.startswith(("cbranch_scc", "cbranch_vcc")):
+                continue        # wave-uniform control (loop tail, plane stores): the surface's own code follows
             if kind.startswith("cbranch_execz") and any(y.startswith("s_andn2_saveexec") for y in ins[:i]):
                 prev = blks[k - 1][1] if k > 0 else []
                 then_out_of_line = any(y.startswith("s_cbranch_execnz") for y in ins[:i] + prev)
