@@ -1184,6 +1184,11 @@ constexpr int kPosOnly = 1;
 // e.g. the spot sweep, whose host evaluates every medium at the group's one wavelength): no per-lane division path,
 // and the ratio stays a scalar operand
 constexpr int kUniMedia = 2;
+// MODE kNoAt: the caller stores no "at" plane (the final-plane kernels: emit_at does nothing) but keeps the full
+// semantics of `after`: the front-side test and a flat's backward exclusion join the final kill of `after` instead of
+// filling the intersection with NaN first -- `after` is all NaN either way (the reference refracts the NaN
+// intersection into an all-NaN ray), one fill instead of three and no copy of the incoming direction
+constexpr int kNoAt = 4;
 template <typename T, int KIND, int GEO = kGeoGeneral, int MODE = 0, typename EmitAt, class G = GuardBranch>
 RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl, EmitAt&& emit_at,
                           Ray<T>& after, G* g = nullptr, T* rxy = nullptr) {
@@ -1205,7 +1210,8 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
         // positions only: a flat's backward exclusion joins the row's final kill (fwd), as a kAxial sphere's root
         // test does; the history steps apply it to the intersection inside to_plane (there the kill's condition is
         // the sign test the phase needs anyway: measured 2 VALU cheaper than a separate flag)
-        hit_and_normal<T, KIND, GEO>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz, (MODE & kPosOnly) != 0 ? &fwd : nullptr);
+        constexpr bool kFold = (MODE & kPosOnly) != 0 || ((MODE & kNoAt) != 0 && KIND == FLAT);
+        hit_and_normal<T, KIND, GEO>(s, r, n1, iwl, g, rxy, ri, Nx, Ny, Nz, kFold ? &fwd : nullptr);
         if constexpr (KIND == PLANE_MIRROR) {
             emit_at(ri);
             after = reflect(ri, Nx, Ny, Nz, g);
@@ -1218,6 +1224,8 @@ RTPB_HD void surface_step(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, c
                 // NaN first (6 register fills issued on every path) -- `after` is all NaN either way, and so is every
                 // later position of the row (its next intersection reads a NaN direction); emit_at is not called
                 ok = !front_side_fails<GEO, true>(r, s) && fwd;
+            } else if constexpr ((MODE & kNoAt) != 0) {
+                ok = !front_side_fails<GEO, false>(r, s) && fwd;           // joins the final kill (kNoAt)
             } else {
                 kill_if(front_side_fails<GEO, false>(r, s), ri);
                 emit_at(ri);
@@ -1346,11 +1354,12 @@ RTPB_HD void dispatch_code(int code, Step&& step) {
     }
 }
 
-template <typename T, bool WITH_LENS = true, typename EmitAt, class G = GuardBranch>
+// MODE: 0 (both planes of the surface) or kNoAt (final-plane kernels: no "at" plane)
+template <typename T, bool WITH_LENS = true, int MODE = 0, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
                                     EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
     dispatch_kind<WITH_LENS>(s, [&](auto kind, auto geo) {
-        surface_step<T, decltype(kind)::value, decltype(geo)::value>(s, r, n1, n2, iwl, emit_at, after, g);
+        surface_step<T, decltype(kind)::value, decltype(geo)::value, MODE>(s, r, n1, n2, iwl, emit_at, after, g);
     });
 }
 

@@ -156,10 +156,11 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         for (int s = 0; s < a.nsurf; s += 2) {
             const T n_mid = mat_n(mats + s + 1);
             Ray<T> mid;
-            propagate_surface_emit<T, kLens>(surface(s), r, n_cur, n_mid, iwl, [](const Ray<T>&) {}, mid);
+            propagate_surface_emit<T, kLens, kNoAt>(surface(s), r, n_cur, n_mid, iwl, [](const Ray<T>&) {}, mid);
             if (s + 1 < a.nsurf) {
                 const T n_next = mat_n(mats + s + 2);
-                propagate_surface_emit<T, kLens>(surface(s + 1), mid, n_mid, n_next, iwl, [](const Ray<T>&) {}, r);
+                propagate_surface_emit<T, kLens, kNoAt>(surface(s + 1), mid, n_mid, n_next, iwl, [](const Ray<T>&) {},
+                                                        r);
                 n_cur = n_next;
             } else {
                 r = mid;
