@@ -217,6 +217,16 @@ int rtpb_plan_create(const rtpb_surface* surfaces, int32_t nsurf, const rtpb_mat
     }
     if (!p->table.empty()) p->feat |= (p->table.size() / 2 <= static_cast<size_t>(kLdsTablePairs)) ? 4 : 8;
     if (g_indexed_materials.load()) build_indexed(*p);
+    if (p->feat == 1) {
+        // PerfectLens code and plain media: the lens-and-flat variant when every surface takes one of its 4 forms
+        bool lens_flat = true;
+        for (const rtpb_surface& s : p->surf) {
+            const DevSurface<double> d = lower_surface(s);
+            lens_flat = lens_flat && (d.kind == FLAT || d.kind == PERFECT_LENS) &&
+                        surface_geo(d.kind, d.rcp_ok) != kGeoGeneral;
+        }
+        if (lens_flat) p->feat |= 32;
+    }
     blob_layout<double>(*p);
     *plan_out = p;
     return RTPB_OK;

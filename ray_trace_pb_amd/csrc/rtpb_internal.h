@@ -87,9 +87,12 @@ struct TraceArgs {
 // layouts, the tuning knobs and the plan's features (rtpb_trace_kernel.h).  The plan-feature variants come in two
 // groups compiled in separate translation units (rtpb_trace_<tin>_<ts>.hip: group 0, ..._g1.hip: group 1), so the
 // eight largest compiles of the library run in parallel.
-// group 0: feat 0, 1, 4, 5 (constant / Sellmeier / LDS-table media, with or without PerfectLens code);
-// group 1: feat 16, 17 (indexed materials) and 15 (everything)
-constexpr int trace_feat_group(int feat) { return (feat == 0 || feat == 1 || feat == 4 || feat == 5) ? 0 : 1; }
+// group 0: feat 0, 1, 4, 5 (constant / Sellmeier / LDS-table media, with or without PerfectLens code) and 33 (feat 1
+// with only PerfectLens and Flat surfaces in the kAxial / kPlaneXZ forms); group 1: feat 16, 17 (indexed materials)
+// and 15 (everything)
+constexpr int trace_feat_group(int feat) {
+    return (feat == 0 || feat == 1 || feat == 4 || feat == 5 || feat == 33) ? 0 : 1;
+}
 template <typename TIN, typename TS, int GROUP>
 hipError_t launch_trace_group(const TraceArgs<TIN, TS>& a, int il, int ol, int feat, hipStream_t st);
 #define RTPB_TRACE_GROUP_EXTERN(TI, TS)                                                                             \
@@ -427,7 +430,8 @@ struct rtpb_plan {
     std::vector<double> table;          // (wavelength, n) pairs of every TABLE material
     // kernel features needed: 1 = PerfectLens, 2 = POLY6 material, 4 = TABLE materials whose table fits
     // the kernel's LDS copy (kLdsTablePairs), 8 = TABLE materials read from global memory, 16 = indexed
-    // materials (replaces 4 / 8; see kLdsIndexedDoubles)
+    // materials (replaces 4 / 8; see kLdsIndexedDoubles), 32 = with 1 and nothing else: every surface a PerfectLens
+    // or a Flat in the kAxial / kPlaneXZ form (dispatch_kind's kKindsLensFlat)
     int feat = 0;
     std::vector<double> itab;           // indexed materials: [nkeys keys][(nsurf+1) x nkeys n][nsurf x nkeys ratios]
     int32_t nkeys = 0;

@@ -1283,15 +1283,33 @@ RTPB_HD int surface_geo(int kind, int32_t rcp_ok) {
     return (kind != SPHERE && (rcp_ok & kPlaneXZ)) ? kGeoXZ : kGeoGeneral;
 }
 
+// The surface forms a kernel variant compiles (rtpb_plan::feat bit 32): every form, or only PerfectLens and Flat
+// steps in the kAxial / kPlaneXZ forms (C4's OPM and the other PerfectLens relays: 4 arms instead of 9 -- fewer
+// values to merge after the switch, measured 292.8 -> 272.1 VALU per ray-surface on C4, profiles/r06/x)
+constexpr int kKindsAll = 0;
+constexpr int kKindsLensFlat = 1;
+
 // Any surface: a wave-uniform switch on the kind and the geometry form: calls
 // step(integral_constant<int, KIND>, integral_constant<int, GEO>).  WITH_LENS = false compiles the
 // PerfectLens case out (lower register pressure -> 5 waves/SIMD instead of 4); only valid for plans
-// without PerfectLens surfaces (rtpb_plan::feat).
-template <bool WITH_LENS, typename T, typename Step>
+// without PerfectLens surfaces (rtpb_plan::feat).  KINDS = kKindsLensFlat: only valid for plans whose feat has bit 32.
+template <bool WITH_LENS, int KINDS = kKindsAll, typename T, typename Step>
 RTPB_HD void dispatch_kind(const DevSurface<T>& s, Step&& step) {
     using std::integral_constant;
     const int kind = s.kind;
     const int geo = surface_geo(kind, s.rcp_ok);
+    if constexpr (KINDS == kKindsLensFlat) {
+        static_assert(WITH_LENS, "the lens-and-flat variant carries the PerfectLens code");
+        if (kind == PERFECT_LENS) {
+            if (geo == kGeoAxial) step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoAxial>());
+            else step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoXZ>());
+        } else if (geo == kGeoAxial) {
+            step(integral_constant<int, FLAT>(), integral_constant<int, kGeoAxial>());
+        } else {
+            step(integral_constant<int, FLAT>(), integral_constant<int, kGeoXZ>());
+        }
+        return;
+    }
     if (WITH_LENS && kind == PERFECT_LENS) {
         if constexpr (WITH_LENS) {
             if (geo == kGeoAxial) step(integral_constant<int, PERFECT_LENS>(), integral_constant<int, kGeoAxial>());
@@ -1354,11 +1372,11 @@ RTPB_HD void dispatch_code(int code, Step&& step) {
     }
 }
 
-// MODE: 0 (both planes of the surface) or kNoAt (final-plane kernels: no "at" plane)
-template <typename T, bool WITH_LENS = true, int MODE = 0, typename EmitAt, class G = GuardBranch>
+// MODE: 0 (both planes of the surface) or kNoAt (final-plane kernels: no "at" plane); KINDS: dispatch_kind's
+template <typename T, bool WITH_LENS = true, int MODE = 0, int KINDS = kKindsAll, typename EmitAt, class G = GuardBranch>
 RTPB_HD void propagate_surface_emit(const DevSurface<T>& s, const Ray<T>& r, T n1, T n2, const Rcp<T>& iwl,
                                     EmitAt&& emit_at, Ray<T>& after, G* g = nullptr) {
-    dispatch_kind<WITH_LENS>(s, [&](auto kind, auto geo) {
+    dispatch_kind<WITH_LENS, KINDS>(s, [&](auto kind, auto geo) {
         surface_step<T, decltype(kind)::value, decltype(geo)::value, MODE>(s, r, n1, n2, iwl, emit_at, after, g);
     });
 }

@@ -64,6 +64,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
     // LDS tile, fewer live registers (the C5 / spot-diagram and focus-finding mode)
     constexpr bool kFinal = (STORE & 8) != 0;
     constexpr bool kLens = (FEAT & 1) != 0, kPoly = (FEAT & 2) != 0;
+    constexpr int kKinds = (FEAT & 32) != 0 ? kKindsLensFlat : kKindsAll;    // rtpb_plan::feat bit 32
     constexpr bool kTabLds = (FEAT & 12) == 4, kTabGlobal = (FEAT & 8) != 0, kIdx = (FEAT & 16) != 0;
     extern __shared__ double lds_table[];                // FEAT bit 2: the plan's (wavelength, n) pairs;
                                                          // FEAT bit 4: the indexed-material table
@@ -156,10 +157,10 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
         for (int s = 0; s < a.nsurf; s += 2) {
             const T n_mid = mat_n(mats + s + 1);
             Ray<T> mid;
-            propagate_surface_emit<T, kLens, kNoAt>(surface(s), r, n_cur, n_mid, iwl, [](const Ray<T>&) {}, mid);
+            propagate_surface_emit<T, kLens, kNoAt, kKinds>(surface(s), r, n_cur, n_mid, iwl, [](const Ray<T>&) {}, mid);
             if (s + 1 < a.nsurf) {
                 const T n_next = mat_n(mats + s + 2);
-                propagate_surface_emit<T, kLens, kNoAt>(surface(s + 1), mid, n_mid, n_next, iwl, [](const Ray<T>&) {},
+                propagate_surface_emit<T, kLens, kNoAt, kKinds>(surface(s + 1), mid, n_mid, n_next, iwl, [](const Ray<T>&) {},
                                                         r);
                 n_cur = n_next;
             } else {
@@ -212,7 +213,7 @@ void trace_kernel(TraceArgs<TIN, TS> a) {
                 if (valid && st_at) store_ray<TS, OUT_LAYOUT>(out + off_at, i, a.out_fs, at);
             }
         };
-        propagate_surface_emit<T, kLens>(surface(s), in, n_in, n_next, iwl, emit_at, res);
+        propagate_surface_emit<T, kLens, 0, kKinds>(surface(s), in, n_in, n_next, iwl, emit_at, res);
         if constexpr (kXchg) {
             if (st_after) xchg_flush<kNT>(out + off_after, ray0, a.n, lane, res);
         } else if constexpr (kStaged) {
@@ -268,6 +269,7 @@ hipError_t launch_one(const TraceArgs<TI, T>& a, int feat, hipStream_t st) {
         case 1: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(1), 1>(a, st);
         case 4: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(4), 4>(a, st);
         case 5: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(5), 5>(a, st);
+        case 33: return launch_w<TI, T, IL, OL, ST, RTPB_WPE(33), 33>(a, st);
         default: return hipErrorInvalidValue;                                // another group's feature set
         }
     } else {
