@@ -135,6 +135,39 @@ def test_tuning_variants_bitwise(knob):
         C.check(lib.rtpb_set_tuning(knob[0].encode(), default))
 
 
+def test_lens_and_flat_kernel_variant_every_store_path():
+    """C4's OPM -- PerfectLens and Flat surfaces in the axial and x-z forms only, so its plan takes the lens-and-flat
+    kernel variant (rtpb_plan::feat 33, dispatch_kind's kKindsLensFlat) -- through every store path of that variant:
+    float64 / float32 storage, AOS and SoA, the final plane, a plane subset, float32 input and each tuning knob."""
+    system, m0, m1, rays, ref = build_case("c4_opm")
+    assert {type(s).__name__ for s in system.surfaces} == {"PerfectLens", "FlatSurface"}
+    r32 = rays.astype(np.float32)
+    ref32 = oracle(system, m0, m1, r32.astype(np.float64))
+    lib = C.lib()
+
+    def run(r, **kw):
+        out = system.ray_trace(torch.from_numpy(r).to(DEV), m0, m1, **kw)
+        return out.cpu().numpy()
+
+    def sweep(tag):
+        for r, exp in ((rays, ref), (r32, ref32)):
+            for dt, e in (("float64", exp), ("float32", exp.astype(np.float32))):
+                assert same_bits(run(r, dtype=dt), e), (tag, r.dtype, dt, "all")
+                assert same_bits(run(r, dtype=dt, planes="final")[0], e[-1]), (tag, r.dtype, dt, "final")
+                assert same_bits(run(r, dtype=dt, planes=[1, 5, 22]), e[[1, 5, 22]]), (tag, r.dtype, dt, "subset")
+                soa = run(r, dtype=dt, layout="soa")
+                assert same_bits(np.swapaxes(soa, 1, 2), e), (tag, r.dtype, dt, "soa")
+
+    sweep("default")
+    for knob, value, default in (("aos_staging", 0, 1), ("aos_staging", 2, 1), ("nt_stores", 0, 1),
+                                 ("stage_input", 1, 0)):
+        C.check(lib.rtpb_set_tuning(knob.encode(), value))
+        try:
+            sweep(f"{knob}={value}")
+        finally:
+            C.check(lib.rtpb_set_tuning(knob.encode(), default))
+
+
 def test_sharded_host_trace_is_bitwise_equal():
     """Ray sharding over devices (here: two shards on GPU 0) gives exactly the unsharded history."""
     system, m0, m1, rays, ref = build_case("stress")
